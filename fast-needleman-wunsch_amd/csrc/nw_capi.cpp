@@ -1,0 +1,325 @@
+// nw_capi.cpp -- C ABI of libnwhip.so (declared in include/nw_hip.h).
+//
+// Owns device workspace (hand-off granules, row-character packs, ticket/error
+// words, ramp scratch), validates shapes, and launches the gfx950 kernels of
+// nw_fill.hip.  The one-shot nw_fill() is the drop-in path used by the
+// reference-signature TU (dropin/needleman-wunsch-hip.cpp); it replaces the
+// reference fills' needlemanWunsch() (serial.cpp:4, sentinel-mt.cpp:4,
+// idxarray-mt.cpp:4) as called from driver.cpp:28.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+
+#include "nw_hip.h"
+#include "nw_internal.h"
+
+struct nw_ctx {
+    int device = 0;
+    int cus = 256;
+    uint64_t *gran = nullptr;
+    size_t gran_cap = 0;  // bytes
+    uint32_t *rowpack = nullptr;
+    size_t rowpack_cap = 0;
+    int32_t *scratch = nullptr;
+    size_t scratch_cap = 0;
+    uint32_t *ctrl = nullptr;  // 4 words
+    uint32_t tagbase = 1;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    int last_waves = 0;
+    int last_strips = 0;
+};
+
+namespace {
+
+constexpr int kWavesPerCU = 4;  // 33 KB LDS per single-wave workgroup -> 4 per CU
+
+inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+#define NW_HIP_TRY(expr)                                                         \
+    do {                                                                         \
+        hipError_t e_ = (expr);                                                  \
+        if (e_ != hipSuccess) {                                                  \
+            std::fprintf(stderr, "libnwhip: %s failed: %s (%s:%d)\n", #expr,     \
+                         hipGetErrorString(e_), __FILE__, __LINE__);             \
+            return e_ == hipErrorOutOfMemory ? NW_ERR_OOM : NW_ERR_HIP;          \
+        }                                                                        \
+    } while (0)
+
+int grow(void **p, size_t *cap, size_t need, bool zero) {
+    if (need <= *cap) return NW_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    need = (size_t)round_up((int64_t)need, 1 << 21);
+    NW_HIP_TRY(hipMalloc(p, need));
+    if (zero) NW_HIP_TRY(hipMemset(*p, 0, need));
+    *cap = need;
+    return NW_OK;
+}
+
+struct Shape {
+    int64_t nRows, nCols, nstrips, nblocks, waves, M, gstride;
+};
+
+Shape make_shape(int64_t n1, int64_t n2, int32_t waves_req, int cus) {
+    Shape s;
+    s.nRows = n2 + 1;
+    s.nCols = n1 + 1;
+    s.nstrips = (s.nCols + nw::kWave - 1) / nw::kWave;
+    s.nblocks = (s.nRows + nw::kWave - 1) / nw::kWave;
+    int64_t w = waves_req > 0 ? waves_req : (int64_t)kWavesPerCU * cus;
+    s.waves = std::max<int64_t>(1, std::min<int64_t>(w, s.nstrips));
+    // Strip p publishes into slot p % M.  When strip p is claimed, every strip
+    // <= p - waves has finished, so M = waves + 1 slots never alias a live one.
+    s.M = std::min<int64_t>(s.nstrips, s.waves + 1);
+    s.gstride = s.nblocks * nw::kWave;
+    return s;
+}
+
+bool valid_params(const nw_params *p) {
+    if (!p) return false;
+    if (p->mode != NW_MODE_NW) return false;
+    // keep every intermediate far from int32 overflow (|score| < 2^29)
+    const int32_t lim = 1 << 12;
+    return std::abs(p->match) < lim && std::abs(p->mismatch) < lim && std::abs(p->gap) < lim;
+}
+
+}  // namespace
+
+extern "C" {
+
+void nw_params_default(nw_params *p) {
+    if (!p) return;
+    std::memset(p, 0, sizeof(*p));
+    p->match = 1;      // needleman-wunsch.hpp:11
+    p->mismatch = 0;   // needleman-wunsch.hpp:12
+    p->gap = -1;       // needleman-wunsch.hpp:13
+    p->mode = NW_MODE_NW;
+    p->waves = 0;
+    p->device = -1;
+}
+
+const char *nw_strerror(int status) {
+    switch (status) {
+        case NW_OK: return "ok";
+        case NW_ERR_ARG: return "invalid argument";
+        case NW_ERR_HIP: return "HIP runtime error";
+        case NW_ERR_OOM: return "out of device memory";
+        case NW_ERR_TIMEOUT: return "in-kernel hand-off watchdog expired";
+        case NW_ERR_NODEVICE: return "no gfx950 device";
+        case NW_ERR_UNSUPPORTED: return "unsupported";
+        default: return "unknown status";
+    }
+}
+
+const char *nw_version(void) {
+    static char buf[128];
+    std::snprintf(buf, sizeof buf, "libnwhip gfx950 %s", nw::kernel_variant());
+    return buf;
+}
+
+int64_t nw_table_pitch(int64_t n1) { return round_up(n1 + 1, nw::kWave); }
+
+int64_t nw_table_bytes(int64_t n1, int64_t n2) {
+    return round_up(n2 + 1, nw::kWave) * nw_table_pitch(n1) * (int64_t)sizeof(int32_t);
+}
+
+int64_t nw_ctx_workspace_bytes(int64_t n1, int64_t n2, int32_t waves) {
+    Shape s = make_shape(n1, n2, waves, 256);
+    return s.M * s.gstride * 8 + nw::rowpack_len((int32_t)s.nblocks) * 4 +
+           s.waves * nw::kScratchWords * 4 + 16;
+}
+
+int nw_ctx_create(int device, nw_ctx **out) {
+    if (!out) return NW_ERR_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return NW_ERR_NODEVICE;
+    if (device < 0) NW_HIP_TRY(hipGetDevice(&device));
+    if (device >= ndev) return NW_ERR_ARG;
+    NW_HIP_TRY(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    NW_HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        std::fprintf(stderr, "libnwhip: device %d is %s, kernels are built for gfx950\n", device,
+                     prop.gcnArchName);
+        return NW_ERR_NODEVICE;
+    }
+    nw_ctx *c = new nw_ctx();
+    c->device = device;
+    c->cus = prop.multiProcessorCount;
+    if (hipMalloc(&c->ctrl, 16) != hipSuccess || hipMemset(c->ctrl, 0, 16) != hipSuccess ||
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+        nw_ctx_destroy(c);
+        return NW_ERR_HIP;
+    }
+    *out = c;
+    return NW_OK;
+}
+
+void nw_ctx_destroy(nw_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->gran) (void)hipFree(c->gran);
+    if (c->rowpack) (void)hipFree(c->rowpack);
+    if (c->scratch) (void)hipFree(c->scratch);
+    if (c->ctrl) (void)hipFree(c->ctrl);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    delete c;
+}
+
+int nw_fill_device_async(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *d_s2,
+                         int64_t n2, const nw_params *p, int32_t *d_t, int64_t pitch,
+                         void *stream) {
+    if (!c || !d_t || n1 < 0 || n2 < 0 || n1 >= INT32_MAX || n2 >= INT32_MAX) return NW_ERR_ARG;
+    if ((n1 > 0 && !d_s1) || (n2 > 0 && !d_s2)) return NW_ERR_ARG;
+    if (!valid_params(p)) return NW_ERR_ARG;
+    if (pitch < nw_table_pitch(n1) || pitch % nw::kWave != 0) return NW_ERR_ARG;
+    if (((uintptr_t)d_t & 255u) != 0) return NW_ERR_ARG;
+    NW_HIP_TRY(hipSetDevice(c->device));
+    const Shape s = make_shape(n1, n2, p->waves, c->cus);
+    if (s.nstrips > INT32_MAX / 2 || s.nblocks > INT32_MAX / 2) return NW_ERR_ARG;
+
+    int st;
+    // Hand-off granules.  (Re)allocation zeroes them; tags are then unique per
+    // (launch, strip) as long as tagbase does not wrap -- re-zero when it would.
+    const size_t gran_need = (size_t)(s.M * s.gstride) * sizeof(uint64_t);
+    if (gran_need > c->gran_cap) {
+        if ((st = grow((void **)&c->gran, &c->gran_cap, gran_need, true)) != NW_OK) return st;
+        c->tagbase = 1;
+    }
+    if ((uint64_t)c->tagbase + (uint64_t)s.nstrips + 2u >= 0xFFFFFFF0ull) {
+        NW_HIP_TRY(hipMemsetAsync(c->gran, 0, c->gran_cap, (hipStream_t)stream));
+        c->tagbase = 1;
+    }
+    const int64_t qlen = nw::rowpack_len((int32_t)s.nblocks);
+    if ((st = grow((void **)&c->rowpack, &c->rowpack_cap, (size_t)qlen * 4, false)) != NW_OK)
+        return st;
+    if ((st = grow((void **)&c->scratch, &c->scratch_cap,
+                   (size_t)s.waves * nw::kScratchWords * 4, false)) != NW_OK)
+        return st;
+
+    NW_HIP_TRY(hipMemsetAsync(c->ctrl, 0, 16, (hipStream_t)stream));
+    const uint8_t *s2u = n2 > 0 ? (const uint8_t *)d_s2 : (const uint8_t *)c->ctrl;
+    if (nw::launch_rowpack(s2u, n2, 0, c->rowpack, qlen, stream) != hipSuccess) return NW_ERR_HIP;
+
+    nw::FillArgs a;
+    std::memset(&a, 0, sizeof a);
+    a.table = d_t;
+    a.pitch = pitch;
+    a.rowpack = c->rowpack;
+    a.s1 = n1 > 0 ? (const uint8_t *)d_s1 : (const uint8_t *)c->ctrl;
+    a.n1 = n1;
+    a.n2 = n2;
+    a.row0 = 0;
+    a.nstrips = (int32_t)s.nstrips;
+    a.nblocks = (int32_t)s.nblocks;
+    a.gran = c->gran;
+    a.gstride = s.gstride;
+    a.M = (int32_t)s.M;
+    a.tagbase = c->tagbase;
+    a.ctrl = c->ctrl;
+    a.top = nullptr;
+    a.scratch = c->scratch;
+    a.match = p->match;
+    a.mismatch = p->mismatch;
+    a.gap = p->gap;
+    if (nw::launch_fill(a, (int)s.waves, stream) != hipSuccess) return NW_ERR_HIP;
+    c->tagbase += (uint32_t)s.nstrips + 1u;
+    c->last_waves = (int)s.waves;
+    c->last_strips = (int)s.nstrips;
+    return NW_OK;
+}
+
+int nw_ctx_status(nw_ctx *c, void *stream) {
+    if (!c) return NW_ERR_ARG;
+    NW_HIP_TRY(hipSetDevice(c->device));
+    uint32_t w[4] = {0, 0, 0, 0};
+    NW_HIP_TRY(hipMemcpyAsync(w, c->ctrl, sizeof w, hipMemcpyDeviceToHost, (hipStream_t)stream));
+    NW_HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    return w[1] != 0 ? NW_ERR_TIMEOUT : NW_OK;
+}
+
+int nw_fill_device(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *d_s2, int64_t n2,
+                   const nw_params *p, int32_t *d_t, int64_t pitch, void *stream,
+                   nw_result *out) {
+    if (!c) return NW_ERR_ARG;
+    NW_HIP_TRY(hipSetDevice(c->device));
+    if (out) NW_HIP_TRY(hipEventRecord(c->ev0, (hipStream_t)stream));
+    int st = nw_fill_device_async(c, d_s1, n1, d_s2, n2, p, d_t, pitch, stream);
+    if (st != NW_OK || !out) return st;
+    NW_HIP_TRY(hipEventRecord(c->ev1, (hipStream_t)stream));
+    st = nw_ctx_status(c, stream);
+    std::memset(out, 0, sizeof *out);
+    out->status = st;
+    float ms = 0.f;
+    NW_HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    out->kernel_ms = ms;
+    out->cells = n1 * n2;
+    out->table_bytes = (double)(n1 + 1) * (double)(n2 + 1) * 4.0;
+    out->strips = c->last_strips;
+    out->waves = c->last_waves;
+    int32_t score = 0;
+    NW_HIP_TRY(hipMemcpy(&score, d_t + n2 * pitch + n1, 4, hipMemcpyDeviceToHost));
+    out->score = score;
+    return st;
+}
+
+int nw_fill(const int8_t *s1, int64_t n1, const int8_t *s2, int64_t n2, const nw_params *p,
+            int32_t *host_t, nw_result *out) {
+    nw_params def;
+    if (!p) {
+        nw_params_default(&def);
+        p = &def;
+    }
+    if (n1 < 0 || n2 < 0 || (n1 > 0 && !s1) || (n2 > 0 && !s2)) return NW_ERR_ARG;
+    // one context per device per process, created on first use
+    static std::mutex mu;
+    static nw_ctx *ctxs[64] = {nullptr};
+    int dev = p->device;
+    if (dev < 0 && hipGetDevice(&dev) != hipSuccess) return NW_ERR_NODEVICE;
+    if (dev < 0 || dev >= 64) return NW_ERR_ARG;
+    std::lock_guard<std::mutex> lock(mu);
+    if (!ctxs[dev]) {
+        int st = nw_ctx_create(dev, &ctxs[dev]);
+        if (st != NW_OK) return st;
+    }
+    nw_ctx *c = ctxs[dev];
+    NW_HIP_TRY(hipSetDevice(dev));
+    const int64_t pitch = nw_table_pitch(n1);
+    int8_t *d_s1 = nullptr, *d_s2 = nullptr;
+    int32_t *d_t = nullptr;
+    nw_result r;
+    std::memset(&r, 0, sizeof r);
+    int st = NW_OK;
+    hipError_t e = hipMalloc(&d_t, (size_t)nw_table_bytes(n1, n2));
+    if (e != hipSuccess) return e == hipErrorOutOfMemory ? NW_ERR_OOM : NW_ERR_HIP;
+    if (hipMalloc(&d_s1, (size_t)std::max<int64_t>(n1, 1)) != hipSuccess ||
+        hipMalloc(&d_s2, (size_t)std::max<int64_t>(n2, 1)) != hipSuccess) {
+        st = NW_ERR_OOM;
+    }
+    if (st == NW_OK && n1 > 0 && hipMemcpy(d_s1, s1, (size_t)n1, hipMemcpyHostToDevice) != hipSuccess)
+        st = NW_ERR_HIP;
+    if (st == NW_OK && n2 > 0 && hipMemcpy(d_s2, s2, (size_t)n2, hipMemcpyHostToDevice) != hipSuccess)
+        st = NW_ERR_HIP;
+    if (st == NW_OK) st = nw_fill_device(c, d_s1, n1, d_s2, n2, p, d_t, pitch, nullptr, &r);
+    if (st == NW_OK && host_t) {
+        const size_t w = (size_t)(n1 + 1) * sizeof(int32_t);
+        if (hipMemcpy2D(host_t, w, d_t, (size_t)pitch * 4, w, (size_t)(n2 + 1),
+                        hipMemcpyDeviceToHost) != hipSuccess)
+            st = NW_ERR_HIP;
+    }
+    (void)hipFree(d_t);
+    if (d_s1) (void)hipFree(d_s1);
+    if (d_s2) (void)hipFree(d_s2);
+    r.status = st;
+    if (out) *out = r;
+    return st;
+}
+
+}  // extern "C"

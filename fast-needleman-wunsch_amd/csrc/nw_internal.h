@@ -1,0 +1,44 @@
+// nw_internal.h -- shared between the HIP kernels (nw_fill.hip) and the C-ABI
+// layer (nw_capi.cpp).  Not part of the public ABI (include/nw_hip.h is).
+#pragma once
+#include <stdint.h>
+
+namespace nw {
+
+constexpr int kWave = 64;          // lanes per wavefront = columns per strip
+constexpr int kRing = 128;         // rows held by the LDS staging ring (2 blocks of 64)
+constexpr int kQOff = 64;          // rowpack index offset (lane l reads index 4g - l)
+constexpr int32_t kNeg = -(1 << 29);  // "minus infinity" fed left of column 0
+constexpr int kScratchWords = kWave * kWave + 2 * kWave;  // per workgroup (16.5 KB)
+
+// Everything one launch of the strip-sweep kernel needs.  Plain POD, passed by
+// value as the kernel argument.
+struct FillArgs {
+    int32_t *table;            // device table, row-major, row pitch `pitch` (int32 elems)
+    int64_t pitch;             // multiple of 64 (256-B aligned rows)
+    const uint32_t *rowpack;   // rowpack[x + kQOff] = B[x] | B[x+1]<<8 | B[x+2]<<16 | B[x+3]<<24,
+                               //   B[x] = s2[x-1] for 1 <= x <= n2, else 0
+    const uint8_t *s1;         // n1 column characters
+    int64_t n1, n2;            // nCols = n1 + 1, nRows = n2 + 1
+    int64_t row0;              // global row index of local row 0 (0 for a whole table)
+    int32_t nstrips;           // ceil(nCols / 64)
+    int32_t nblocks;           // ceil(nRows / 64)
+    uint64_t *gran;            // right-boundary hand-off granules [M][gstride] {tag:32 | value:32}
+    int64_t gstride;           // granules per slot = 64 * nblocks
+    int32_t M;                 // number of slots (>= waves + 1, or nstrips)
+    uint32_t tagbase;          // strip p publishes tag tagbase + p + 1
+    uint32_t *ctrl;            // [0] strip ticket, [1] error word, [2..3] spare
+    const int32_t *top;        // optional device row 0 (nCols values) for row bands; NULL = j*gap
+    int32_t *scratch;          // per-workgroup dummy flush target: grid * kScratchWords int32
+    int32_t match, mismatch, gap;
+    int32_t pad;
+};
+
+// Launch helpers implemented in nw_fill.hip.  Return hipError_t as int.
+int launch_rowpack(const uint8_t *d_s2, int64_t n2, int64_t row0, uint32_t *d_q, int64_t qlen,
+                   void *stream);
+int launch_fill(const FillArgs &a, int grid, void *stream);
+int64_t rowpack_len(int32_t nblocks);
+const char *kernel_variant();
+
+}  // namespace nw

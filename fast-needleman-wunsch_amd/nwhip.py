@@ -1,0 +1,236 @@
+"""ctypes binding of libnwhip.so (include/nw_hip.h) -- the MI355X NW fill.
+
+This is the Python-side mirror of the reference's fill plugin interface
+(`needlemanWunsch(dnaArray s1, dnaArray s2, int* t)`, src/serial/serial.cpp:4):
+`fill(s1, s2)` returns the full (n2+1) x (n1+1) int32 table in the reference
+layout, `score(s1, s2)` only t[n2][n1] (what src/common/driver.cpp:35 prints).
+Device-resident variants take torch tensors and never leave HBM.
+
+There is no CPU fallback: if build/libnwhip.so is missing or no gfx950 device is
+visible, every call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "libnwhip.so")
+
+NW_OK, NW_ERR_ARG, NW_ERR_HIP, NW_ERR_OOM, NW_ERR_TIMEOUT, NW_ERR_NODEVICE, NW_ERR_UNSUPPORTED = range(7)
+
+# every symbol include/nw_hip.h declares (checked by tests/test_host.py)
+EXPORTS = ["nw_params_default", "nw_strerror", "nw_version", "nw_fill", "nw_table_pitch",
+           "nw_table_bytes", "nw_ctx_create", "nw_ctx_destroy", "nw_ctx_workspace_bytes",
+           "nw_fill_device", "nw_fill_device_async", "nw_ctx_status", "nw_read_bdna", "nw_free",
+           "nw_synth_bdna"]
+
+
+class NwParams(ctypes.Structure):
+    _fields_ = [("match", ctypes.c_int32), ("mismatch", ctypes.c_int32), ("gap", ctypes.c_int32),
+                ("mode", ctypes.c_int32), ("waves", ctypes.c_int32), ("device", ctypes.c_int32),
+                ("flags", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class NwResult(ctypes.Structure):
+    _fields_ = [("score", ctypes.c_int32), ("status", ctypes.c_int32), ("cells", ctypes.c_int64),
+                ("kernel_ms", ctypes.c_double), ("table_bytes", ctypes.c_double),
+                ("strips", ctypes.c_int32), ("waves", ctypes.c_int32)]
+
+
+class NwError(RuntimeError):
+    def __init__(self, status: int, what: str = ""):
+        self.status = status
+        super().__init__(f"libnwhip {what}: {strerror(status)} ({status})")
+
+
+_lib = None
+_i8p = ctypes.POINTER(ctypes.c_int8)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+
+
+def lib() -> ctypes.CDLL:
+    """Load build/libnwhip.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise FileNotFoundError(f"{LIB_PATH} missing: run `make -C fast-needleman-wunsch_amd` "
+                                "(or __graft_entry__.build()); there is no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    L.nw_params_default.argtypes = [ctypes.POINTER(NwParams)]
+    L.nw_params_default.restype = None
+    L.nw_strerror.argtypes = [ctypes.c_int]
+    L.nw_strerror.restype = ctypes.c_char_p
+    L.nw_version.restype = ctypes.c_char_p
+    L.nw_fill.argtypes = [_i8p, ctypes.c_int64, _i8p, ctypes.c_int64, ctypes.POINTER(NwParams),
+                          _i32p, ctypes.POINTER(NwResult)]
+    L.nw_table_pitch.argtypes = [ctypes.c_int64]
+    L.nw_table_pitch.restype = ctypes.c_int64
+    L.nw_table_bytes.argtypes = [ctypes.c_int64, ctypes.c_int64]
+    L.nw_table_bytes.restype = ctypes.c_int64
+    L.nw_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+    L.nw_ctx_destroy.argtypes = [ctypes.c_void_p]
+    L.nw_ctx_destroy.restype = None
+    L.nw_ctx_workspace_bytes.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int32]
+    L.nw_ctx_workspace_bytes.restype = ctypes.c_int64
+    dev_args = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
+                ctypes.POINTER(NwParams), ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+    L.nw_fill_device.argtypes = dev_args + [ctypes.POINTER(NwResult)]
+    L.nw_fill_device_async.argtypes = dev_args
+    L.nw_ctx_status.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    L.nw_read_bdna.argtypes = [ctypes.c_char_p, ctypes.POINTER(_i8p), ctypes.POINTER(ctypes.c_int64)]
+    L.nw_free.argtypes = [ctypes.c_void_p]
+    L.nw_free.restype = None
+    L.nw_synth_bdna.argtypes = [ctypes.c_uint64, ctypes.c_int64, _i8p]
+    L.nw_synth_bdna.restype = None
+    _lib = L
+    return L
+
+
+def strerror(status: int) -> str:
+    try:
+        return lib().nw_strerror(status).decode()
+    except FileNotFoundError:
+        return str(status)
+
+
+def version() -> str:
+    return lib().nw_version().decode()
+
+
+@dataclass
+class Scheme:
+    """Runtime replacement of needleman-wunsch.hpp:11-13 (MATCH, MISMATCH, GAP)."""
+    match: int = 1
+    mismatch: int = 0
+    gap: int = -1
+
+
+def params(scheme=(1, 0, -1), waves: int = 0, device: int = -1) -> NwParams:
+    if isinstance(scheme, Scheme):
+        scheme = (scheme.match, scheme.mismatch, scheme.gap)
+    p = NwParams()
+    lib().nw_params_default(ctypes.byref(p))
+    p.match, p.mismatch, p.gap = (int(x) for x in scheme)
+    p.waves = int(waves)
+    p.device = int(device)
+    return p
+
+
+def _seq(s) -> np.ndarray:
+    if isinstance(s, (bytes, bytearray)):
+        return np.frombuffer(bytes(s), dtype=np.int8).copy()
+    return np.ascontiguousarray(np.asarray(s, dtype=np.int8))
+
+
+def fill(s1, s2, scheme=(1, 0, -1), waves: int = 0, device: int = -1):
+    """Full table in the reference layout ((n2+1) x (n1+1) int32) + NwResult."""
+    a, b = _seq(s1), _seq(s2)
+    t = np.empty((b.size + 1, a.size + 1), dtype=np.int32)
+    r = NwResult()
+    p = params(scheme, waves, device)
+    st = lib().nw_fill(a.ctypes.data_as(_i8p), a.size, b.ctypes.data_as(_i8p), b.size,
+                       ctypes.byref(p), t.ctypes.data_as(_i32p), ctypes.byref(r))
+    if st != NW_OK:
+        raise NwError(st, "nw_fill")
+    return t, r
+
+
+def score(s1, s2, scheme=(1, 0, -1), waves: int = 0, device: int = -1) -> int:
+    a, b = _seq(s1), _seq(s2)
+    r = NwResult()
+    p = params(scheme, waves, device)
+    st = lib().nw_fill(a.ctypes.data_as(_i8p), a.size, b.ctypes.data_as(_i8p), b.size,
+                       ctypes.byref(p), None, ctypes.byref(r))
+    if st != NW_OK:
+        raise NwError(st, "nw_fill")
+    return int(r.score)
+
+
+def table_pitch(n1: int) -> int:
+    return int(lib().nw_table_pitch(n1))
+
+
+def table_rows(n2: int) -> int:
+    return (n2 + 1 + 63) // 64 * 64
+
+
+def read_bdna(path: str) -> np.ndarray:
+    """readSequence semantics (src/common/helper.cpp:3-25)."""
+    buf = _i8p()
+    n = ctypes.c_int64()
+    st = lib().nw_read_bdna(path.encode(), ctypes.byref(buf), ctypes.byref(n))
+    if st != NW_OK:
+        raise FileNotFoundError(path)
+    out = np.ctypeslib.as_array(buf, shape=(n.value,)).copy() if n.value else np.zeros(0, np.int8)
+    lib().nw_free(buf)
+    return out
+
+
+def synth(seed: int, n: int) -> np.ndarray:
+    out = np.empty(n, dtype=np.int8)
+    lib().nw_synth_bdna(seed, n, out.ctypes.data_as(_i8p))
+    return out
+
+
+class Context:
+    """Device-resident fills on torch tensors (table stays in HBM)."""
+
+    def __init__(self, device: int = 0):
+        self._h = ctypes.c_void_p()
+        st = lib().nw_ctx_create(device, ctypes.byref(self._h))
+        if st != NW_OK:
+            raise NwError(st, "nw_ctx_create")
+        self.device = device
+
+    def close(self):
+        if self._h:
+            lib().nw_ctx_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def alloc_table(n1: int, n2: int, device="cuda"):
+        import torch
+        return torch.empty((table_rows(n2), table_pitch(n1)), dtype=torch.int32, device=device)
+
+    def fill(self, d_s1, d_s2, table, scheme=(1, 0, -1), waves: int = 0, stream=None,
+             sync: bool = True):
+        """d_s1/d_s2: int8/uint8 CUDA tensors; table: from alloc_table.  Returns NwResult
+        when sync, else None (launch only)."""
+        import torch
+        n1, n2 = int(d_s1.numel()), int(d_s2.numel())
+        assert table.dtype == torch.int32 and table.is_contiguous()
+        assert table.shape[0] >= table_rows(n2) and table.shape[1] == table_pitch(n1)
+        if stream is None:
+            stream = torch.cuda.current_stream(table.device)
+        sp = ctypes.c_void_p(stream.cuda_stream)
+        p = params(scheme, waves, self.device)
+        args = (self._h, ctypes.c_void_p(d_s1.data_ptr() if n1 else 0), n1,
+                ctypes.c_void_p(d_s2.data_ptr() if n2 else 0), n2, ctypes.byref(p),
+                ctypes.c_void_p(table.data_ptr()), table.shape[1], sp)
+        if sync:
+            r = NwResult()
+            st = lib().nw_fill_device(*args, ctypes.byref(r))
+            if st != NW_OK:
+                raise NwError(st, "nw_fill_device")
+            return r
+        st = lib().nw_fill_device_async(*args)
+        if st != NW_OK:
+            raise NwError(st, "nw_fill_device_async")
+        return None
+
+    def status(self, stream=None) -> int:
+        import torch
+        if stream is None:
+            stream = torch.cuda.current_stream()
+        return int(lib().nw_ctx_status(self._h, ctypes.c_void_p(stream.cuda_stream)))

@@ -1,0 +1,140 @@
+/*
+ * nw_hip.h -- C ABI of libnwhip.so, the MI355X (gfx950) Needleman-Wunsch fill.
+ *
+ * This is the drop-in boundary for the reference's fill plugins.  The reference
+ * selects a fill at link time: every fill TU defines
+ *
+ *     void needlemanWunsch(dnaArray s1, dnaArray s2, int* t);
+ *       src/serial/serial.cpp:4          (serial -- the oracle)
+ *       src/sentinel/sentinel-mt.cpp:4   (sentinel-mt)
+ *       src/idxarray/idxarray-mt.cpp:4   (idxarray-mt)
+ *
+ * and textually includes src/common/driver.cpp (its main(), :1-40).  The
+ * MI355X drop-in TU (fast-needleman-wunsch_amd/dropin/needleman-wunsch-hip.cpp)
+ * defines that same C++ symbol and forwards to nw_fill() below.  Everything in
+ * this header is plain C: pointers, sizes, PODs -- no HIP or torch types.
+ *
+ * Table layout (reference contract, serial.cpp:6-7,21-31): nRows = n2 + 1
+ * (s2 "down the side"), nCols = n1 + 1 (s1 "across the top"), cell (i, j) at
+ * t[i * nCols + j], int32.  On the device the library may use a row pitch
+ * >= nCols (see nw_table_pitch); host copies always use the reference layout.
+ */
+#ifndef NW_HIP_H
+#define NW_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* status codes (the reference's fill is void and cannot fail; the C ABI reports
+ * what the device path can: bad arguments, HIP errors, OOM, a watchdog trip) */
+enum {
+    NW_OK = 0,
+    NW_ERR_ARG = 1,       /* invalid argument (sizes, pitch, alignment, mode)   */
+    NW_ERR_HIP = 2,       /* a HIP runtime call failed                         */
+    NW_ERR_OOM = 3,       /* device allocation failed / table does not fit     */
+    NW_ERR_TIMEOUT = 4,   /* a bounded in-kernel wait expired (never expected) */
+    NW_ERR_NODEVICE = 5,  /* no gfx950 device visible                          */
+    NW_ERR_UNSUPPORTED = 6
+};
+
+enum { NW_MODE_NW = 0 };
+
+/* Runtime replacement for the compile-time constants of
+ * src/common/needleman-wunsch.hpp:11-13 (MATCH 1, MISMATCH 0, GAP -1). */
+typedef struct nw_params {
+    int32_t match;     /* default  1 */
+    int32_t mismatch;  /* default  0 */
+    int32_t gap;       /* default -1 */
+    int32_t mode;      /* NW_MODE_NW */
+    int32_t waves;     /* persistent strip workers (0 = auto)            */
+    int32_t device;    /* HIP device ordinal, -1 = current device         */
+    int32_t flags;     /* reserved, 0                                     */
+    int32_t reserved;
+} nw_params;
+
+typedef struct nw_result {
+    int32_t score;          /* t[n2][n1] -- what driver.cpp:35 prints     */
+    int32_t status;         /* NW_OK or an error code                     */
+    int64_t cells;          /* n1 * n2 inner cells (GCUPS numerator)      */
+    double kernel_ms;       /* device time of the fill (HIP events)       */
+    double table_bytes;     /* bytes of table stored: 4 * nRows * nCols   */
+    int32_t strips;         /* 64-column strips swept                     */
+    int32_t waves;          /* persistent workers launched                */
+} nw_result;
+
+/* Fill `p` with the reference defaults (1, 0, -1). */
+void nw_params_default(nw_params *p);
+
+/* Human-readable text for a status code. */
+const char *nw_strerror(int status);
+
+/* Library / kernel build identification (gfx target, kernel variant). */
+const char *nw_version(void);
+
+/*
+ * One-shot fill from host buffers (the drop-in path).  Copies s1/s2 to the
+ * device, fills the whole table in HBM, and -- when host_t != NULL -- copies
+ * the table back in the reference layout (nCols-pitched, (n2+1)*(n1+1) ints).
+ * With host_t == NULL only the score is returned.  Returns NW_OK or an error.
+ * Replaces needlemanWunsch() of serial.cpp:4 / sentinel-mt.cpp:4 /
+ * idxarray-mt.cpp:4 (called from driver.cpp:28).
+ */
+int nw_fill(const int8_t *s1, int64_t n1, const int8_t *s2, int64_t n2,
+            const nw_params *p, int32_t *host_t, nw_result *out);
+
+/* Device-resident API ------------------------------------------------------ */
+typedef struct nw_ctx nw_ctx;
+
+/* Row pitch (in int32 elements) the device kernel requires for nCols = n1+1:
+ * a multiple of 64 (256-byte aligned rows). */
+int64_t nw_table_pitch(int64_t n1);
+
+/* Bytes of device memory a table of (n2+1) rows at nw_table_pitch(n1) takes. */
+int64_t nw_table_bytes(int64_t n1, int64_t n2);
+
+/* Create / destroy a context bound to `device` (-1 = current).  The context
+ * owns the hand-off workspace and the strip ticket counter. */
+int nw_ctx_create(int device, nw_ctx **out);
+void nw_ctx_destroy(nw_ctx *ctx);
+
+/* Workspace bytes the context will allocate for this shape (advisory). */
+int64_t nw_ctx_workspace_bytes(int64_t n1, int64_t n2, int32_t waves);
+
+/*
+ * Fill a device-resident table.  d_s1/d_s2: device int8 sequences; d_t: device
+ * table with row pitch `pitch` (>= nw_table_pitch(n1), multiple of 64,
+ * 256-byte aligned base).  `stream` is a hipStream_t (NULL = default stream).
+ * Asynchronous with respect to the host unless out != NULL, in which case the
+ * call synchronises the stream and fills `out` (score read back from HBM).
+ */
+int nw_fill_device(nw_ctx *ctx, const int8_t *d_s1, int64_t n1,
+                   const int8_t *d_s2, int64_t n2, const nw_params *p,
+                   int32_t *d_t, int64_t pitch, void *stream, nw_result *out);
+
+/* Launch-only variant for timing loops: no synchronisation, no readback. */
+int nw_fill_device_async(nw_ctx *ctx, const int8_t *d_s1, int64_t n1,
+                         const int8_t *d_s2, int64_t n2, const nw_params *p,
+                         int32_t *d_t, int64_t pitch, void *stream);
+
+/* Check the in-kernel watchdog word of the last launch (syncs the stream). */
+int nw_ctx_status(nw_ctx *ctx, void *stream);
+
+/* Host helpers ------------------------------------------------------------- */
+
+/* readSequence semantics (src/common/helper.cpp:3-25): every byte of the file,
+ * no stripping.  *out is malloc'ed; free with nw_free().  Returns NW_OK or
+ * NW_ERR_ARG if the file cannot be opened. */
+int nw_read_bdna(const char *path, int8_t **out, int64_t *n);
+void nw_free(void *p);
+
+/* Seeded synthetic sequence: i.i.d. uniform bytes in {1,2,3,4} (SplitMix64). */
+void nw_synth_bdna(uint64_t seed, int64_t n, int8_t *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NW_HIP_H */

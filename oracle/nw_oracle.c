@@ -1,0 +1,240 @@
+/*
+ * oracle/nw_oracle.c -- CPU restatement of the reference Needleman-Wunsch fill.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product path (the HIP library, the
+ * drop-in TU, the driver) links, loads or calls this file.  It is used by
+ * tests/, by __graft_entry__.smoke() as the checker, and by bench.py's
+ * cpu_baseline leg.
+ *
+ * Parity pinning: every function here is checked in tests/test_oracle.py
+ * against golden vectors produced by the reference itself (the unmodified
+ * reference sources compiled into oracle/_ref/ by oracle/Makefile; fixtures
+ * committed under tests/golden/ by tests/golden/make_golden.py).
+ *
+ * Reference being restated (all paths relative to the reference root):
+ *   src/serial/serial.cpp:4-36         nw_oracle_fill            (the oracle proper)
+ *   src/idxarray/idxarray-mt.cpp:4-70  nw_oracle_fill_idxarray   (CPU baseline "port")
+ *   src/mpi/mpi-horz.cpp:4-99 +
+ *   src/mpi/mpi-horz-driver.cpp:31-32  nw_oracle_band_layout / nw_oracle_fill_band
+ *   src/common/needleman-wunsch.hpp:11-16  scoring constants -> runtime parameters
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <stdatomic.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* serial.cpp:29-30: a - (((a - b) >> SHIFTBITS) & (a - b)).  Evaluated in
+ * wrapping 32-bit arithmetic so that the C restatement has no undefined
+ * behaviour; equal to max(a, b) whenever a - b does not overflow. */
+static inline int32_t ref_max(int32_t a, int32_t b) {
+    int32_t d = (int32_t)((uint32_t)a - (uint32_t)b);
+    return (int32_t)((uint32_t)a - (uint32_t)((d >> 31) & d));
+}
+
+/* serial.cpp:23-24: m = -(s1[j-1] == s2[i-1]); (m & MATCH) | (~m & MISMATCH) */
+static inline int32_t ref_sub(int8_t a, int8_t b, int32_t match, int32_t mismatch) {
+    int32_t m = -(int32_t)(a == b);
+    return (m & match) | (~m & mismatch);
+}
+
+static inline int32_t ref_cell(int32_t diag, int32_t up, int32_t left,
+                               int8_t a, int8_t b, int32_t match,
+                               int32_t mismatch, int32_t gap) {
+    int32_t x = (int32_t)((uint32_t)diag + (uint32_t)ref_sub(a, b, match, mismatch));
+    int32_t y = (int32_t)((uint32_t)up + (uint32_t)gap);
+    int32_t z = (int32_t)((uint32_t)left + (uint32_t)gap);
+    x = ref_max(x, y);
+    return ref_max(x, z);
+}
+
+/*
+ * Full-table fill, row-major, nRows = n2 + 1 (s2 "down the side"),
+ * nCols = n1 + 1 (s1 "across the top"); cell (i, j) at t[i * pitch + j]
+ * (pitch >= nCols; the reference layout is pitch == nCols).
+ * serial.cpp:6-7 (shape), :12-17 (boundaries), :21-33 (row-major sweep).
+ */
+void nw_oracle_fill(const int8_t *s1, int64_t n1, const int8_t *s2, int64_t n2,
+                    int32_t match, int32_t mismatch, int32_t gap,
+                    int32_t *t, int64_t pitch) {
+    const int64_t nRows = n2 + 1, nCols = n1 + 1;
+    if (pitch < nCols) pitch = nCols;
+    t[0] = 0;
+    for (int64_t j = 1; j < nCols; ++j) t[j] = (int32_t)((uint32_t)t[j - 1] + (uint32_t)gap);
+    for (int64_t i = 1; i < nRows; ++i)
+        t[i * pitch] = (int32_t)((uint32_t)t[(i - 1) * pitch] + (uint32_t)gap);
+    for (int64_t i = 1; i < nRows; ++i) {
+        const int32_t *up = t + (i - 1) * pitch;
+        int32_t *row = t + i * pitch;
+        const int8_t b = s2[i - 1];
+        int32_t left = row[0];
+        for (int64_t j = 1; j < nCols; ++j) {
+            left = ref_cell(up[j - 1], up[j], left, s1[j - 1], b, match, mismatch, gap);
+            row[j] = left;
+        }
+    }
+}
+
+/*
+ * Score-only restatement in O(n1) memory: same recurrence, two rolling rows.
+ * Optionally returns the last row (n1 + 1 values), the last column (n2 + 1
+ * values) and per-row checksums (sum and column-weighted sum, both mod 2^64)
+ * so that tables too large for host RAM can still be compared row by row.
+ * Returns t[n2][n1].
+ */
+int32_t nw_oracle_score(const int8_t *s1, int64_t n1, const int8_t *s2, int64_t n2,
+                        int32_t match, int32_t mismatch, int32_t gap,
+                        int32_t *last_row, int32_t *last_col,
+                        uint64_t *row_sum, uint64_t *row_wsum) {
+    const int64_t nRows = n2 + 1, nCols = n1 + 1;
+    int32_t *a = (int32_t *)malloc(sizeof(int32_t) * (size_t)nCols);
+    int32_t *b = (int32_t *)malloc(sizeof(int32_t) * (size_t)nCols);
+    if (!a || !b) { free(a); free(b); return 0; }
+    a[0] = 0;
+    for (int64_t j = 1; j < nCols; ++j) a[j] = (int32_t)((uint32_t)a[j - 1] + (uint32_t)gap);
+    if (last_col) last_col[0] = a[nCols - 1];
+    if (row_sum || row_wsum) {
+        uint64_t s = 0, w = 0;
+        for (int64_t j = 0; j < nCols; ++j) {
+            s += (uint64_t)(int64_t)a[j];
+            w += (uint64_t)(int64_t)a[j] * (uint64_t)(j + 1);
+        }
+        if (row_sum) row_sum[0] = s;
+        if (row_wsum) row_wsum[0] = w;
+    }
+    for (int64_t i = 1; i < nRows; ++i) {
+        const int8_t c = s2[i - 1];
+        int32_t left = (int32_t)((uint32_t)a[0] + (uint32_t)gap);
+        b[0] = left;
+        for (int64_t j = 1; j < nCols; ++j) {
+            left = ref_cell(a[j - 1], a[j], left, s1[j - 1], c, match, mismatch, gap);
+            b[j] = left;
+        }
+        if (last_col) last_col[i] = b[nCols - 1];
+        if (row_sum || row_wsum) {
+            uint64_t s = 0, w = 0;
+            for (int64_t j = 0; j < nCols; ++j) {
+                s += (uint64_t)(int64_t)b[j];
+                w += (uint64_t)(int64_t)b[j] * (uint64_t)(j + 1);
+            }
+            if (row_sum) row_sum[i] = s;
+            if (row_wsum) row_wsum[i] = w;
+        }
+        int32_t *tmp = a; a = b; b = tmp;
+    }
+    int32_t score = a[nCols - 1];
+    if (last_row) memcpy(last_row, a, sizeof(int32_t) * (size_t)nCols);
+    free(a);
+    free(b);
+    return score;
+}
+
+/*
+ * idxarray-mt restatement (src/idxarray/idxarray-mt.cpp:4-70): rows are dealt
+ * cyclically to threads (:43); idx[i] is row i's loop variable j (:44); row i
+ * may compute column j once idx[i-1] > j (:50-56).  The reference relies on
+ * x86 TSO + an asm spin; the restatement uses C11 acquire/release atomics.
+ * The counters stay adjacent 8-byte words, as in the reference (:8), so the
+ * false sharing that dominates its run time is preserved.  Used only as the
+ * CPU baseline ("port") in bench.py and cross-checked against nw_oracle_fill.
+ */
+void nw_oracle_fill_idxarray(const int8_t *s1, int64_t n1, const int8_t *s2, int64_t n2,
+                             int32_t match, int32_t mismatch, int32_t gap,
+                             int32_t *t, int nthreads) {
+    const int64_t nRows = n2 + 1, nCols = n1 + 1;
+    _Atomic int64_t *idx = (_Atomic int64_t *)malloc(sizeof(int64_t) * (size_t)nRows);
+    if (!idx) return;
+    for (int64_t i = 0; i < nRows; ++i) atomic_init(&idx[i], 0);
+    atomic_store_explicit(&idx[0], nCols, memory_order_relaxed);     /* :17-21 */
+    t[0] = 0;                                                          /* :24-28 */
+    for (int64_t j = 1; j < nCols; ++j) t[j] = (int32_t)((uint32_t)t[j - 1] + (uint32_t)gap);
+    for (int64_t i = 1; i < nRows; ++i)                                /* :31-37 */
+        t[nCols * i] = (int32_t)((uint32_t)t[nCols * (i - 1)] + (uint32_t)gap);
+    if (nthreads <= 0) nthreads = 1;
+#pragma omp parallel num_threads(nthreads)
+    {
+        int64_t tnum = 0, nth = 1;
+#ifdef _OPENMP
+        tnum = omp_get_thread_num();
+        nth = omp_get_num_threads();
+#endif
+        for (int64_t i = tnum + 1; i < nRows; i += nth) {              /* :43 */
+            const int8_t b = s2[i - 1];
+            int32_t *row = t + i * nCols;
+            const int32_t *up = row - nCols;
+            int32_t left = row[0];
+            for (int64_t j = 1; j < nCols; ++j) {
+                while (atomic_load_explicit(&idx[i - 1], memory_order_acquire) <= j) { }
+                left = ref_cell(up[j - 1], up[j], left, s1[j - 1], b, match, mismatch, gap);
+                row[j] = left;
+                atomic_store_explicit(&idx[i], j + 1, memory_order_release);
+            }
+            atomic_store_explicit(&idx[i], nCols, memory_order_release);
+        }
+    }
+    free((void *)idx);
+}
+
+/*
+ * Row-band partition of src/mpi/mpi-horz-driver.cpp:31-32 and
+ * src/mpi/mpi-horz.cpp:16: base = (n2+1)/P; band r holds
+ * base + (r > 0) [+ (n2+1) % P on the last rank] rows; its local row 0 is
+ * global row start = base*r - (r > 0) (for r > 0 that row is the halo, i.e.
+ * the last row of band r-1).
+ */
+void nw_oracle_band_layout(int64_t n2, int P, int r, int64_t *nRows_r, int64_t *start_r) {
+    int64_t base = (n2 + 1) / P;
+    int64_t rows = base + (r > 0);
+    if (r == P - 1) rows += (n2 + 1) % P;
+    *nRows_r = rows;
+    *start_r = base * r - (r > 0);
+}
+
+/*
+ * Fill one row band (mpi-horz.cpp:4-99 semantics, without the chunked MPI
+ * pipeline): `halo` is global row start_r (nCols values) for r > 0 and is
+ * ignored for r == 0; band rows are written to t[k * nCols + j], k = 0 is the
+ * halo / global row 0.  Column 0 is (k + start) * GAP (:19).
+ */
+void nw_oracle_fill_band(const int8_t *s1, int64_t n1, const int8_t *s2, int64_t n2,
+                         int32_t match, int32_t mismatch, int32_t gap,
+                         int P, int r, const int32_t *halo, int32_t *t) {
+    int64_t nRows, start;
+    const int64_t nCols = n1 + 1;
+    (void)n2;
+    nw_oracle_band_layout(n2, P, r, &nRows, &start);
+    for (int64_t i = 0; i < nRows; ++i) t[i * nCols] = (int32_t)((i + start) * (int64_t)gap);
+    if (r == 0) {
+        for (int64_t j = 0; j < nCols; ++j) t[j] = (int32_t)(j * (int64_t)gap);
+    } else {
+        memcpy(t, halo, sizeof(int32_t) * (size_t)nCols);
+    }
+    for (int64_t i = 1; i < nRows; ++i) {
+        const int8_t b = s2[start + i - 1];
+        int32_t *row = t + i * nCols;
+        const int32_t *up = row - nCols;
+        int32_t left = row[0];
+        for (int64_t j = 1; j < nCols; ++j) {
+            left = ref_cell(up[j - 1], up[j], left, s1[j - 1], b, match, mismatch, gap);
+            row[j] = left;
+        }
+    }
+}
+
+/* Seeded synthetic .bdna generator: i.i.d. uniform bytes in
+ * {1,2,3,4} from a SplitMix64 stream.  Shared with the product-side generator
+ * in fast-needleman-wunsch_amd/csrc/nw_bdna.cpp, which must produce the same
+ * bytes (checked in tests/test_host.py). */
+void nw_oracle_synth(uint64_t seed, int64_t n, int8_t *out) {
+    uint64_t x = seed;
+    for (int64_t i = 0; i < n; ++i) {
+        x += 0x9E3779B97F4A7C15ull;
+        uint64_t z = x;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z ^= z >> 31;
+        out[i] = (int8_t)(1 + (z >> 62));
+    }
+}

@@ -1,0 +1,162 @@
+"""ctypes binding for the CPU oracle -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() (as the checker) and bench.py's
+cpu_baseline leg import this module.  The product path never does.
+
+Wraps oracle/liboracle.so (the C restatement in oracle/nw_oracle.c) and, when
+present, the reference's own fills compiled into oracle/_ref/ by
+oracle/Makefile (those export the reference C++ entry point
+`needlemanWunsch(dnaArray, dnaArray, int*)`, src/serial/serial.cpp:4).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF_DIR = os.path.join(HERE, "_ref")
+
+# scheme name -> (match, mismatch, gap); "shipped" = needleman-wunsch.hpp:11-13
+SCHEMES = {"shipped": (1, 0, -1), "mm1": (1, -1, -1), "p3": (2, -1, -2)}
+
+_i8p = ctypes.POINTER(ctypes.c_int8)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_lib = None
+
+
+def build() -> None:
+    """Compile liboracle.so (and oracle/_ref when /root/reference exists)."""
+    subprocess.run(["make", "-s", "-C", HERE, "all"], check=True)
+    if os.path.isdir("/root/reference/src"):
+        subprocess.run(["make", "-s", "-C", HERE, "ref"], check=True)
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        path = os.path.join(HERE, "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        L = ctypes.CDLL(path)
+        L.nw_oracle_fill.argtypes = [_i8p, ctypes.c_int64, _i8p, ctypes.c_int64,
+                                     ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                     _i32p, ctypes.c_int64]
+        L.nw_oracle_fill.restype = None
+        L.nw_oracle_score.argtypes = [_i8p, ctypes.c_int64, _i8p, ctypes.c_int64,
+                                      ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                      _i32p, _i32p, _u64p, _u64p]
+        L.nw_oracle_score.restype = ctypes.c_int32
+        L.nw_oracle_fill_idxarray.argtypes = [_i8p, ctypes.c_int64, _i8p, ctypes.c_int64,
+                                              ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                              _i32p, ctypes.c_int]
+        L.nw_oracle_fill_idxarray.restype = None
+        L.nw_oracle_band_layout.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                                            ctypes.POINTER(ctypes.c_int64),
+                                            ctypes.POINTER(ctypes.c_int64)]
+        L.nw_oracle_fill_band.argtypes = [_i8p, ctypes.c_int64, _i8p, ctypes.c_int64,
+                                          ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                          ctypes.c_int, ctypes.c_int, _i32p, _i32p]
+        L.nw_oracle_synth.argtypes = [ctypes.c_uint64, ctypes.c_int64, _i8p]
+        _lib = L
+    return _lib
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t)
+
+
+def _seq(s) -> np.ndarray:
+    a = np.ascontiguousarray(np.frombuffer(bytes(s), dtype=np.int8) if isinstance(s, (bytes, bytearray))
+                             else np.asarray(s, dtype=np.int8))
+    if a.size == 0:
+        a = np.zeros(1, dtype=np.int8)[:0]
+    return a
+
+
+def fill(s1, s2, scheme=(1, 0, -1)) -> np.ndarray:
+    """Full table, reference layout (n2+1, n1+1) int32 (serial.cpp:4-36)."""
+    a, b = _seq(s1), _seq(s2)
+    t = np.empty((b.size + 1, a.size + 1), dtype=np.int32)
+    lib().nw_oracle_fill(_p(a, _i8p), a.size, _p(b, _i8p), b.size, *scheme, _p(t, _i32p), a.size + 1)
+    return t
+
+
+def fill_idxarray(s1, s2, scheme=(1, 0, -1), nthreads=8) -> np.ndarray:
+    a, b = _seq(s1), _seq(s2)
+    t = np.empty((b.size + 1, a.size + 1), dtype=np.int32)
+    lib().nw_oracle_fill_idxarray(_p(a, _i8p), a.size, _p(b, _i8p), b.size, *scheme, _p(t, _i32p), nthreads)
+    return t
+
+
+def score(s1, s2, scheme=(1, 0, -1), want_rows=False):
+    """Linear-memory score.  With want_rows: (score, last_row, last_col, row_sum, row_wsum)."""
+    a, b = _seq(s1), _seq(s2)
+    L = lib()
+    if not want_rows:
+        return int(L.nw_oracle_score(_p(a, _i8p), a.size, _p(b, _i8p), b.size, *scheme,
+                                     None, None, None, None))
+    lr = np.empty(a.size + 1, dtype=np.int32)
+    lc = np.empty(b.size + 1, dtype=np.int32)
+    rs = np.empty(b.size + 1, dtype=np.uint64)
+    rw = np.empty(b.size + 1, dtype=np.uint64)
+    sc = L.nw_oracle_score(_p(a, _i8p), a.size, _p(b, _i8p), b.size, *scheme,
+                           _p(lr, _i32p), _p(lc, _i32p), _p(rs, _u64p), _p(rw, _u64p))
+    return int(sc), lr, lc, rs, rw
+
+
+def band_layout(n2: int, P: int, r: int):
+    nr, st = ctypes.c_int64(), ctypes.c_int64()
+    lib().nw_oracle_band_layout(n2, P, r, ctypes.byref(nr), ctypes.byref(st))
+    return nr.value, st.value
+
+
+def fill_band(s1, s2, P, r, halo, scheme=(1, 0, -1)) -> np.ndarray:
+    a, b = _seq(s1), _seq(s2)
+    nr, _ = band_layout(b.size, P, r)
+    t = np.empty((nr, a.size + 1), dtype=np.int32)
+    h = np.ascontiguousarray(halo, dtype=np.int32) if halo is not None else np.zeros(a.size + 1, np.int32)
+    lib().nw_oracle_fill_band(_p(a, _i8p), a.size, _p(b, _i8p), b.size, *scheme, P, r,
+                              _p(h, _i32p), _p(t, _i32p))
+    return t
+
+
+def synth(seed: int, n: int) -> np.ndarray:
+    out = np.empty(n, dtype=np.int8)
+    lib().nw_oracle_synth(seed, n, _p(out, _i8p))
+    return out
+
+
+def row_checksums(t: np.ndarray):
+    """(sum, column-weighted sum) per row, mod 2^64 -- same definition as nw_oracle_score."""
+    t64 = t.astype(np.int64).view(np.uint64)
+    w = np.arange(1, t.shape[1] + 1, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        return t64.sum(axis=1, dtype=np.uint64), (t64 * w).sum(axis=1, dtype=np.uint64)
+
+
+# ---------------------------------------------------------------- reference (_ref)
+class DnaArray(ctypes.Structure):
+    """src/common/helper.hpp:9-12 -- {int size; int8_t* dna;} passed by value."""
+    _fields_ = [("size", ctypes.c_int), ("dna", _i8p)]
+
+
+def ref_available(name: str = "libref_serial.so") -> bool:
+    return os.path.exists(os.path.join(REF_DIR, name))
+
+
+def ref_fill(s1, s2, lib_name="libref_serial.so") -> np.ndarray:
+    """Run the reference's own needlemanWunsch (compiled from its sources) on s1 x s2."""
+    L = ctypes.CDLL(os.path.join(REF_DIR, lib_name))
+    fn = getattr(L, "_Z15needlemanWunsch8dnaArrayS_Pi")
+    fn.argtypes = [DnaArray, DnaArray, _i32p]
+    fn.restype = None
+    a, b = _seq(s1), _seq(s2)
+    a_buf = np.ascontiguousarray(a) if a.size else np.zeros(1, np.int8)
+    b_buf = np.ascontiguousarray(b) if b.size else np.zeros(1, np.int8)
+    t = np.zeros((b.size + 1, a.size + 1), dtype=np.int32)
+    fn(DnaArray(a.size, _p(a_buf, _i8p)), DnaArray(b.size, _p(b_buf, _i8p)), _p(t, _i32p))
+    return t

@@ -1,0 +1,170 @@
+"""GPU parity: the gfx950 fill vs the reference's own outputs and the oracle.
+
+Everything here calls through the C ABI (libnwhip.so) -- the host path
+(nw_fill, reference table layout) and the device-resident path
+(nw_fill_device, table kept in HBM).  Bar: bit-exact int32.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import nwhip
+import oracle
+from conftest import GOLDEN, PKG, bdna_path
+
+pytestmark = pytest.mark.gpu
+SCHEMES = oracle.SCHEMES
+TINY = ["small", "small_rev", "t", "debug"]
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as _t
+    if not _t.cuda.is_available():
+        pytest.skip("no GPU")
+    return _t
+
+
+@pytest.fixture(scope="module")
+def ctx(torch):
+    c = nwhip.Context(0)
+    yield c
+    c.close()
+
+
+def device_fill(torch, ctx, s1, s2, scheme=(1, 0, -1), waves=0):
+    d1 = torch.from_numpy(np.ascontiguousarray(s1)).cuda()
+    d2 = torch.from_numpy(np.ascontiguousarray(s2)).cuda()
+    tab = nwhip.Context.alloc_table(s1.size, s2.size)
+    r = ctx.fill(d1, d2, tab, scheme, waves=waves)
+    assert r.status == 0
+    return tab, r
+
+
+def device_row_checksums(torch, tab, n_rows, n_cols, chunk=1024):
+    """(sum, column-weighted sum) per row, mod 2^64 -- oracle.row_checksums on the GPU."""
+    w = torch.arange(1, n_cols + 1, dtype=torch.int64, device=tab.device)
+    rs, rw = [], []
+    for r0 in range(0, n_rows, chunk):
+        r1 = min(n_rows, r0 + chunk)
+        t64 = tab[r0:r1, :n_cols].to(torch.int64)
+        rs.append(t64.sum(dim=1).cpu())
+        rw.append((t64 * w).sum(dim=1).cpu())
+    return (torch.cat(rs).numpy().view(np.uint64), torch.cat(rw).numpy().view(np.uint64))
+
+
+# ------------------------------------------------------------------ golden (reference)
+@pytest.mark.parametrize("scheme", list(SCHEMES))
+@pytest.mark.parametrize("name", TINY)
+def test_full_table_vs_reference(pair, scheme, name):
+    s1, s2 = pair(name)
+    t, r = nwhip.fill(s1, s2, SCHEMES[scheme])
+    np.testing.assert_array_equal(t, np.load(f"{GOLDEN}/table_{scheme}_{name}.npy"))
+    assert r.score == t[-1, -1]
+
+
+@pytest.mark.parametrize("name", ["small", "t", "debug", "smid", "2gb", "4gb", "8gb", "mid", "big"])
+def test_score_vs_reference(golden, pair, name):
+    s1, s2 = pair(name)
+    for scheme, want in golden["pairs"][name]["scores"].items():
+        assert nwhip.score(s1, s2, SCHEMES[scheme]) == want, (name, scheme)
+
+
+@pytest.mark.parametrize("scheme", list(SCHEMES))
+@pytest.mark.parametrize("name", ["smid", "2gb"])
+def test_rows_vs_reference(torch, ctx, pair, scheme, name):
+    s1, s2 = pair(name)
+    ref = np.load(f"{GOLDEN}/rows_{scheme}_{name}.npz")
+    tab, r = device_fill(torch, ctx, s1, s2, SCHEMES[scheme])
+    n_rows, n_cols = s2.size + 1, s1.size + 1
+    np.testing.assert_array_equal(tab[n_rows - 1, :n_cols].cpu().numpy(), ref["last_row"])
+    np.testing.assert_array_equal(tab[:n_rows, n_cols - 1].cpu().numpy(), ref["last_col"])
+    rs, rw = device_row_checksums(torch, tab, n_rows, n_cols)
+    np.testing.assert_array_equal(rs, ref["row_sum"])
+    np.testing.assert_array_equal(rw, ref["row_wsum"])
+    assert r.score == ref["last_row"][-1]
+
+
+# ------------------------------------------------------------------ oracle, random shapes
+SHAPES = [(0, 0), (0, 1), (1, 0), (1, 1), (2, 3), (63, 63), (64, 64), (65, 65), (63, 65),
+          (127, 1), (1, 127), (128, 129), (129, 128), (191, 200), (255, 257), (1000, 37),
+          (37, 1000), (640, 640), (1500, 1100)]
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("alphabet", ["dna", "bytes"])
+def test_random_vs_oracle(shape, alphabet):
+    rng = np.random.default_rng(shape[0] * 7919 + shape[1] + (alphabet == "bytes"))
+    lo, hi = (1, 5) if alphabet == "dna" else (-128, 128)
+    s1 = rng.integers(lo, hi, shape[0]).astype(np.int8)
+    s2 = rng.integers(lo, hi, shape[1]).astype(np.int8)
+    for scheme in SCHEMES.values():
+        t, _ = nwhip.fill(s1, s2, scheme)
+        np.testing.assert_array_equal(t, oracle.fill(s1, s2, scheme), err_msg=str((shape, scheme)))
+
+
+@pytest.mark.parametrize("scheme", [(3, -2, -2), (1, 1, -1), (0, -1, -3), (5, 0, 0), (2, -3, 1)])
+def test_other_schemes_vs_oracle(scheme):
+    """Runtime scores beyond the reference's #defines (incl. gap 0 and a positive gap)."""
+    rng = np.random.default_rng(11)
+    s1 = rng.integers(1, 5, 700).astype(np.int8)
+    s2 = rng.integers(1, 5, 333).astype(np.int8)
+    t, _ = nwhip.fill(s1, s2, scheme)
+    np.testing.assert_array_equal(t, oracle.fill(s1, s2, scheme))
+
+
+@pytest.mark.parametrize("waves", [1, 2, 3, 5, 8, 17, 64])
+def test_worker_count_independent(torch, ctx, waves):
+    """Few persistent workers -> many strips per worker and hand-off slot reuse
+    (slot = strip % (waves + 1)); results must not depend on it."""
+    rng = np.random.default_rng(waves)
+    s1 = rng.integers(1, 5, 64 * 40 + 17).astype(np.int8)
+    s2 = rng.integers(1, 5, 900).astype(np.int8)
+    want = oracle.fill(s1, s2, (1, -1, -1))
+    tab, r = device_fill(torch, ctx, s1, s2, (1, -1, -1), waves=waves)
+    np.testing.assert_array_equal(tab[:s2.size + 1, :s1.size + 1].cpu().numpy(), want)
+    assert r.waves == min(waves, r.strips)
+
+
+def test_repeated_launches_and_shapes(torch, ctx):
+    """The hand-off tags advance per launch; stale granules of earlier launches
+    (other shapes, same buffers) must never be taken for fresh ones."""
+    rng = np.random.default_rng(5)
+    shapes = [(2000, 300), (300, 2000), (2000, 300), (777, 777), (64 * 50, 128), (2000, 300)]
+    for n1, n2 in shapes:
+        s1 = rng.integers(1, 5, n1).astype(np.int8)
+        s2 = rng.integers(1, 5, n2).astype(np.int8)
+        tab, _ = device_fill(torch, ctx, s1, s2, (1, 0, -1), waves=7)
+        np.testing.assert_array_equal(tab[:n2 + 1, :n1 + 1].cpu().numpy(), oracle.fill(s1, s2))
+
+
+def test_config2_32k_vs_oracle(torch, ctx):
+    """BASELINE config 2: 32k x 32k synthetic (seeds 1, 2), full table in HBM;
+    every row checked through (sum, weighted sum), last row/column exactly."""
+    n = 32768
+    s1, s2 = nwhip.synth(1, n), nwhip.synth(2, n)
+    tab, r = device_fill(torch, ctx, s1, s2, (1, 0, -1))
+    sc, lr, lc, rs, rw = oracle.score(s1, s2, (1, 0, -1), want_rows=True)
+    assert r.score == sc
+    np.testing.assert_array_equal(tab[n, :n + 1].cpu().numpy(), lr)
+    np.testing.assert_array_equal(tab[:n + 1, n].cpu().numpy(), lc)
+    grs, grw = device_row_checksums(torch, tab, n + 1, n + 1)
+    np.testing.assert_array_equal(grs, rs)
+    np.testing.assert_array_equal(grw, rw)
+
+
+# ------------------------------------------------------------------ drop-in CLI
+@pytest.mark.parametrize("drv,name,want", [("nw_driver", "small", 2), ("nw_driver", "t", 17),
+                                           ("nw_driver", "debug", 27), ("nw_driver", "smid", 5839),
+                                           ("nw_driver_mm1", "small", 2), ("nw_driver_mm1", "t", 6),
+                                           ("nw_driver_mm1", "smid", 3955)])
+def test_dropin_driver_cli(golden, drv, name, want):
+    e = golden["pairs"][name]
+    out = subprocess.run([os.path.join(PKG, "build", drv), bdna_path(e["argv1"]),
+                          bdna_path(e["argv2"])], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    lines = out.stdout.strip().split("\n")
+    assert len(lines) == 2 and lines[0].isdigit()          # "<ms>" (driver.cpp:33)
+    assert lines[1] == f"Score: {want}"                      # driver.cpp:35

@@ -1,0 +1,117 @@
+"""CPU: the C-ABI library builds, loads and exports every symbol include/nw_hip.h
+declares; host helpers match the oracle; no silent CPU fallback without a GPU."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import nwhip
+import oracle
+from conftest import ROOT, bdna_path, read_bdna
+
+HEADER = os.path.join(ROOT, "include", "nw_hip.h")
+
+
+def header_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b(nw_\w+)\s*\(", text, flags=re.M)
+    return sorted(set(names))
+
+
+def test_header_declares_expected_api():
+    assert header_functions() == sorted(nwhip.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol():
+    out = subprocess.run(["nm", "-D", "--defined-only", nwhip.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    syms = {line.split()[-1] for line in out.splitlines() if line.strip()}
+    missing = [s for s in header_functions() if s not in syms]
+    assert not missing, missing
+    lib = nwhip.lib()
+    for s in header_functions():
+        assert hasattr(lib, s)
+
+
+def test_kernel_code_object_is_gfx950():
+    data = open(nwhip.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data
+
+
+def test_dropin_driver_exports_reference_plugin_symbol():
+    drv = os.path.join(ROOT, "fast-needleman-wunsch_amd", "build", "nw_driver")
+    out = subprocess.run(["nm", drv], capture_output=True, text=True, check=True).stdout
+    # the reference fills' entry point, src/serial/serial.cpp:4
+    assert "_Z15needlemanWunsch8dnaArrayS_Pi" in out
+
+
+def test_pitch_and_bytes():
+    assert nwhip.table_pitch(0) == 64
+    assert nwhip.table_pitch(63) == 64
+    assert nwhip.table_pitch(64) == 128
+    assert nwhip.lib().nw_table_bytes(262144, 262144) == (262145 + 63) // 64 * 64 * 262208 * 4
+
+
+def test_default_params_are_reference_constants():
+    p = nwhip.params()
+    assert (p.match, p.mismatch, p.gap) == (1, 0, -1)   # needleman-wunsch.hpp:11-13
+
+
+@pytest.mark.parametrize("seed,n", [(1, 0), (1, 1000), (2, 4097), (12345, 10)])
+def test_synth_matches_oracle(seed, n):
+    a = nwhip.synth(seed, n)
+    np.testing.assert_array_equal(a, oracle.synth(seed, n))
+    if n:
+        assert set(np.unique(a)) <= {1, 2, 3, 4}
+
+
+@pytest.mark.parametrize("name", ["small1.bdna", "t2.bdna", "smid1.bdna"])
+def test_read_bdna_is_readsequence(name):
+    np.testing.assert_array_equal(nwhip.read_bdna(bdna_path(name)), read_bdna(name))
+
+
+def test_read_bdna_missing_file():
+    with pytest.raises(FileNotFoundError):
+        nwhip.read_bdna("/nonexistent/x.bdna")
+
+
+def test_read_bdna_keeps_every_byte(tmp_path):
+    p = tmp_path / "x.bdna"
+    raw = bytes([1, 2, 10, 0, 255, 3, 13])   # newline / zero / 0xFF are kept (helper.cpp:9-13)
+    p.write_bytes(raw)
+    np.testing.assert_array_equal(nwhip.read_bdna(str(p)), np.frombuffer(raw, np.int8))
+
+
+def _gpu_visible():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+@pytest.mark.skipif(_gpu_visible(), reason="checks the no-device path")
+def test_no_device_fails_loudly():
+    with pytest.raises(nwhip.NwError) as ei:
+        nwhip.score([1, 2, 3], [1, 2])
+    assert ei.value.status == nwhip.NW_ERR_NODEVICE
+
+
+@pytest.mark.skipif(_gpu_visible(), reason="checks the no-device path")
+def test_dropin_driver_fails_loudly_without_device():
+    drv = os.path.join(ROOT, "fast-needleman-wunsch_amd", "build", "nw_driver")
+    r = subprocess.run([drv, bdna_path("small1.bdna"), bdna_path("small2.bdna")],
+                       capture_output=True, text=True)
+    assert r.returncode == 2
+    assert "libnwhip" in r.stderr
+
+
+def test_driver_cli_argument_errors():
+    drv = os.path.join(ROOT, "fast-needleman-wunsch_amd", "build", "nw_driver")
+    r = subprocess.run([drv, "only-one"], capture_output=True, text=True)
+    assert r.returncode == 1 and "incorrect number of arguments" in r.stdout
+    r = subprocess.run([drv, "/nonexistent/a", "/nonexistent/b"], capture_output=True, text=True)
+    assert r.returncode == 1 and "ERROR: no such file /nonexistent/a" in r.stdout
