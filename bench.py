@@ -1,0 +1,180 @@
+#!/usr/bin/env python3
+"""Benchmark: GCUPS of the N x N Needleman-Wunsch fill on MI355X.
+
+Metric (BASELINE.json): GCUPS = inner cells n1*n2 / fill seconds, bit-exact score.
+A "step" is one complete fill of the table (device-resident: sequences and
+table in HBM before the timed region; nothing copied back inside it).
+
+  N = 1 : BASELINE config 3 -- 262144 x 262144 int32 table (275 GB) on one GPU.
+  N > 1 : row-band partition across ranks (mpi-horz contract); see DESIGN.md.
+
+Prints ONE JSON line on rank 0 (see README / DESIGN.md for field meanings).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "fast-needleman-wunsch_amd")
+sys.path.insert(0, PKG)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--n", type=int, default=262144, help="sequence length (N x N table)")
+    ap.add_argument("--scheme", default="1,0,-1", help="match,mismatch,gap")
+    ap.add_argument("--waves", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-n", type=int, default=65536, help="CPU baseline sample side")
+    return ap.parse_args()
+
+
+def golden_score(n: int, scheme) -> int | None:
+    path = os.path.join(ROOT, "tests", "golden", "synth_scores.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        g = json.load(f)
+    return g.get(f"{n}:{','.join(str(x) for x in scheme)}")
+
+
+def cpu_baseline(n: int, scheme):
+    """Reference serial fill (src/serial/serial.cpp, compiled unmodified into
+    oracle/_ref) on an n x n sample of the same synthetic workload, timed on this
+    host, 1 thread; falls back to the oracle port when _ref is absent."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    import nwhip
+    s1, s2 = nwhip.synth(1, n), nwhip.synth(2, n)
+    lib_name = {(1, 0, -1): "libref_serial.so", (1, -1, -1): "libref_serial_mm1.so",
+                (2, -1, -2): "libref_serial_p3.so"}.get(tuple(scheme))
+    kind = "reference" if lib_name and oracle.ref_available(lib_name) else "port"
+    t0 = time.perf_counter()
+    if kind == "reference":
+        tab = oracle.ref_fill(s1, s2, lib_name)
+        sc = int(tab[-1, -1])
+        del tab
+    else:
+        sc = oracle.score(s1, s2, scheme)
+    dt = time.perf_counter() - t0
+    return {"value": round(n * n / dt / 1e9, 4), "unit": "GCUPS", "cores": 1, "kind": kind,
+            "sample": f"{n}x{n} synthetic seeds 1/2, scheme {tuple(scheme)}, serial.cpp fill "
+                      f"(full table in host RAM), {dt:.2f} s, score {sc}",
+            "host": _host_cpu()}
+
+
+def _host_cpu() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def pmc_traffic(workload: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/)."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    e = d.get(workload)
+    return e.get("hbm_bytes_per_launch") if e else None
+
+
+def run_single(args):
+    import torch
+    import nwhip
+
+    scheme = tuple(int(x) for x in args.scheme.split(","))
+    n = args.n
+    torch.cuda.set_device(0)
+    ctx = nwhip.Context(0)
+    s1 = torch.from_numpy(nwhip.synth(1, n)).cuda()
+    s2 = torch.from_numpy(nwhip.synth(2, n)).cuda()
+    tab = nwhip.Context.alloc_table(n, n)
+    stream = torch.cuda.current_stream()
+
+    for _ in range(args.warmup):
+        ctx.fill(s1, s2, tab, scheme, waves=args.waves, sync=False)
+    torch.cuda.synchronize()
+
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for e0, e1 in evs:
+        e0.record(stream)
+        ctx.fill(s1, s2, tab, scheme, waves=args.waves, sync=False)
+        e1.record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    status = ctx.status()
+    if status != 0:
+        raise RuntimeError(f"fill reported status {status} ({nwhip.strerror(status)})")
+    kms = [e0.elapsed_time(e1) for e0, e1 in evs]
+    score = int(tab[n, n].item())
+    want = golden_score(n, scheme)
+    cells = n * n
+    value = cells * args.steps / wall / 1e9
+    avg_ms = sum(kms) / len(kms)
+    table_bytes = 4.0 * (n + 1) * (n + 1)
+    achieved = table_bytes / (avg_ms * 1e6)  # GB/s, algorithmic bytes (4 B per cell)
+    workload = f"nw_fill_{n}x{n}"
+    out = {
+        "metric": "GCUPS (DP cell updates/s) on NxN NW fill, bit-exact score",
+        "value": round(value, 2),
+        "unit": "GCUPS",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(wall / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic (i.i.d. uniform {1,2,3,4}, seeds 1/2)",
+        "config": {"workload": workload, "n1": n, "n2": n, "scheme": list(scheme),
+                   "table_bytes": int(table_bytes), "layout": "row-major int32, pitch "
+                   f"{nwhip.table_pitch(n)}", "waves": args.waves or "auto", "parallelism": "single GPU"},
+        "score": score,
+        "score_golden": want,
+        "score_ok": (want == score) if want is not None else None,
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                     "traffic": pmc_traffic(workload),
+                     "kernel_ms_avg": round(avg_ms, 3), "bytes_per_launch": int(table_bytes)},
+        "kernel": nwhip.version(),
+    }
+    del tab
+    torch.cuda.empty_cache()
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_n, scheme)
+    print(json.dumps(out), flush=True)
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 or world > 1:
+        from nw_bands import run_bands  # multi-GPU row bands
+        run_bands(args)
+        return
+    run_single(args)
+
+
+if __name__ == "__main__":
+    main()

@@ -31,6 +31,7 @@ struct nw_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int last_waves = 0;
     int last_strips = 0;
+    uint64_t *trace = nullptr;  // debug: per-strip timestamps (nw_debug_set_trace)
 };
 
 namespace {
@@ -226,9 +227,11 @@ int nw_fill_device_async(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t
     a.ctrl = c->ctrl;
     a.top = nullptr;
     a.scratch = c->scratch;
+    a.trace = c->trace;
     a.match = p->match;
     a.mismatch = p->mismatch;
     a.gap = p->gap;
+    a.flags = p->flags;
     if (nw::launch_fill(a, (int)s.waves, stream) != hipSuccess) return NW_ERR_HIP;
     c->tagbase += (uint32_t)s.nstrips + 1u;
     c->last_waves = (int)s.waves;
@@ -320,6 +323,14 @@ int nw_fill(const int8_t *s1, int64_t n1, const int8_t *s2, int64_t n2, const nw
     r.status = st;
     if (out) *out = r;
     return st;
+}
+
+// Debug hook (not part of the public ABI): per-strip trace buffer, device memory
+// of nstrips * 4 uint64 {start, end, slow waits, wait ticks (100 MHz)}; NULL = off.
+int nw_debug_set_trace(nw_ctx *c, void *d_trace) {
+    if (!c) return NW_ERR_ARG;
+    c->trace = (uint64_t *)d_trace;
+    return NW_OK;
 }
 
 }  // extern "C"

@@ -218,14 +218,20 @@ __device__ void process_strip(const FillArgs &A, int32_t *__restrict__ lds, int 
     // same VMEM operations so every path into the next iteration is identical for
     // hipcc's s_waitcnt accounting, and the strip is abandoned at the boundary.
     bool dead = false;
+    uint32_t nslow = 0;
+    uint64_t wticks = 0;
+    const uint64_t tstart = __builtin_amdgcn_s_memrealtime();
     auto iter = [&](int it, const uint32_t(&pk)[16], uint32_t(&pkn)[16], auto ramp) {
         constexpr bool RAMP = decltype(ramp)::value;  // first iteration: no block to flush yet
         if (it < A.nblocks) {
             int32_t fvv = kNeg;
             if (has_left) {
                 if (!__all((uint32_t)(gv >> 32) == tag_in)) {
+                    const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
                     gv = wait_granules_slow(gin + (int64_t)it * 64, tag_in, A.ctrl);
                     dead = !__all((uint32_t)(gv >> 32) == tag_in);
+                    nslow += 1;
+                    wticks += __builtin_amdgcn_s_memrealtime() - w0;
                 }
                 fvv = (int32_t)(uint32_t)gv + gap;
             }
@@ -236,8 +242,13 @@ __device__ void process_strip(const FillArgs &A, int32_t *__restrict__ lds, int 
         run_iter<RAMP, UNIT>(lds, it, lane, pk, a, msp, mmp, gap, tg, tl_old, laddr);
         if constexpr (!RAMP) {
             const int64_t row0 = (int64_t)(it - 1) * 64;
-            flush_block(lds, it - 1, lane, A.table + row0 * A.pitch + (int64_t)p * 64, A.pitch,
-                        gout + row0, tag_out);
+            int32_t *dst = A.table + row0 * A.pitch + (int64_t)p * 64;
+            int64_t pitch = A.pitch;
+            if (A.flags & 1) {  // debug timing mode: keep the stores, drop the HBM traffic
+                dst = A.scratch + (int64_t)blockIdx.x * kScratchWords;
+                pitch = kWave;
+            }
+            flush_block(lds, it - 1, lane, dst, pitch, gout + row0, tag_out);
         } else {
             // Nothing is complete yet.  Issue the same 17 stores into this
             // workgroup's scratch tile so that every path into the steady-state
@@ -254,6 +265,13 @@ __device__ void process_strip(const FillArgs &A, int32_t *__restrict__ lds, int 
         iter(it, pkB, pkA, std::false_type{});
         if (it + 1 >= nit || dead) break;
         iter(it + 1, pkA, pkB, std::false_type{});
+    }
+    if (A.trace != nullptr && lane == 0) {
+        uint64_t *tr = A.trace + (int64_t)p * 4;
+        tr[0] = tstart;
+        tr[1] = __builtin_amdgcn_s_memrealtime();
+        tr[2] = nslow;
+        tr[3] = wticks;
     }
 }
 

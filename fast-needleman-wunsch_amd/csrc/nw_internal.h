@@ -30,8 +30,9 @@ struct FillArgs {
     uint32_t *ctrl;            // [0] strip ticket, [1] error word, [2..3] spare
     const int32_t *top;        // optional device row 0 (nCols values) for row bands; NULL = j*gap
     int32_t *scratch;          // per-workgroup dummy flush target: grid * kScratchWords int32
+    uint64_t *trace;           // optional per-strip trace [nstrips][4]: start, end, slow waits, wait ticks
     int32_t match, mismatch, gap;
-    int32_t pad;
+    int32_t flags;             // debug: bit0 = send table stores to the scratch tile (timing only)
 };
 
 // Launch helpers implemented in nw_fill.hip.  Return hipError_t as int.

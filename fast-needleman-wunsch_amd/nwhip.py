@@ -53,10 +53,18 @@ _i32p = ctypes.POINTER(ctypes.c_int32)
 
 
 def lib() -> ctypes.CDLL:
-    """Load build/libnwhip.so (raises if it has not been built)."""
+    """Load build/libnwhip.so (raises if it has not been built).
+
+    torch (when installed) is imported first: torch and libnwhip share one HIP
+    runtime (libamdhip64.so.7, deduplicated by SONAME), and torch must be the one
+    that loads it or its own device initialisation fails."""
     global _lib
     if _lib is not None:
         return _lib
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
     if not os.path.exists(LIB_PATH):
         raise FileNotFoundError(f"{LIB_PATH} missing: run `make -C fast-needleman-wunsch_amd` "
                                 "(or __graft_entry__.build()); there is no CPU fallback")
@@ -110,7 +118,7 @@ class Scheme:
     gap: int = -1
 
 
-def params(scheme=(1, 0, -1), waves: int = 0, device: int = -1) -> NwParams:
+def params(scheme=(1, 0, -1), waves: int = 0, device: int = -1, flags: int = 0) -> NwParams:
     if isinstance(scheme, Scheme):
         scheme = (scheme.match, scheme.mismatch, scheme.gap)
     p = NwParams()
@@ -118,6 +126,7 @@ def params(scheme=(1, 0, -1), waves: int = 0, device: int = -1) -> NwParams:
     p.match, p.mismatch, p.gap = (int(x) for x in scheme)
     p.waves = int(waves)
     p.device = int(device)
+    p.flags = int(flags)
     return p
 
 
@@ -204,7 +213,7 @@ class Context:
         return torch.empty((table_rows(n2), table_pitch(n1)), dtype=torch.int32, device=device)
 
     def fill(self, d_s1, d_s2, table, scheme=(1, 0, -1), waves: int = 0, stream=None,
-             sync: bool = True):
+             sync: bool = True, flags: int = 0):
         """d_s1/d_s2: int8/uint8 CUDA tensors; table: from alloc_table.  Returns NwResult
         when sync, else None (launch only)."""
         import torch
@@ -214,7 +223,7 @@ class Context:
         if stream is None:
             stream = torch.cuda.current_stream(table.device)
         sp = ctypes.c_void_p(stream.cuda_stream)
-        p = params(scheme, waves, self.device)
+        p = params(scheme, waves, self.device, flags)
         args = (self._h, ctypes.c_void_p(d_s1.data_ptr() if n1 else 0), n1,
                 ctypes.c_void_p(d_s2.data_ptr() if n2 else 0), n2, ctypes.byref(p),
                 ctypes.c_void_p(table.data_ptr()), table.shape[1], sp)
@@ -228,6 +237,13 @@ class Context:
         if st != NW_OK:
             raise NwError(st, "nw_fill_device_async")
         return None
+
+    def set_trace(self, trace_tensor) -> None:
+        """Debug: record {start, end, slow waits, wait ticks} per strip into a
+        uint64/int64 CUDA tensor of nstrips*4 elements (None = off)."""
+        L = lib()
+        L.nw_debug_set_trace.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.nw_debug_set_trace(self._h, ctypes.c_void_p(trace_tensor.data_ptr() if trace_tensor is not None else 0))
 
     def status(self, stream=None) -> int:
         import torch

@@ -15,6 +15,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--sizes", default="32768,65536")
 ap.add_argument("--waves", default="0")
 ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--flags", type=int, default=0)
 args = ap.parse_args()
 ctx = nwhip.Context(0)
 for n in [int(x) for x in args.sizes.split(",")]:
@@ -22,10 +23,10 @@ for n in [int(x) for x in args.sizes.split(",")]:
     s2 = torch.from_numpy(nwhip.synth(2, n)).cuda()
     tab = nwhip.Context.alloc_table(n, n)
     for w in [int(x) for x in args.waves.split(",")]:
-        ctx.fill(s1, s2, tab, waves=w)  # warmup
+        ctx.fill(s1, s2, tab, waves=w, flags=args.flags)  # warmup
         ts = []
         for _ in range(args.reps):
-            r = ctx.fill(s1, s2, tab, waves=w)
+            r = ctx.fill(s1, s2, tab, waves=w, flags=args.flags)
             ts.append(r.kernel_ms)
         ms = min(ts)
         gcups = n * n / (ms * 1e6)

@@ -1,0 +1,45 @@
+"""Per-strip timeline of one fill (debug trace: s_memrealtime at 100 MHz)."""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "fast-needleman-wunsch_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import nwhip  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--n", type=int, default=32768)
+ap.add_argument("--waves", default="0")
+ap.add_argument("--flags", type=int, default=0)
+args = ap.parse_args()
+ctx = nwhip.Context(0)
+n = args.n
+s1 = torch.from_numpy(nwhip.synth(1, n)).cuda()
+s2 = torch.from_numpy(nwhip.synth(2, n)).cuda()
+tab = nwhip.Context.alloc_table(n, n)
+nstrips = (n + 1 + 63) // 64
+tr = torch.zeros(nstrips * 4, dtype=torch.int64, device="cuda")
+for w in [int(x) for x in args.waves.split(",")]:
+    ctx.set_trace(None)
+    r0 = ctx.fill(s1, s2, tab, waves=w, flags=args.flags)
+    ctx.set_trace(tr)
+    r = ctx.fill(s1, s2, tab, waves=w, flags=args.flags)
+    ctx.set_trace(None)
+    t = tr.view(nstrips, 4).cpu().numpy().astype(np.float64)
+    t0 = t[:, 0].min()
+    st = (t[:, 0] - t0) / 100.0   # us
+    en = (t[:, 1] - t0) / 100.0
+    dur = en - st
+    lag = np.diff(st)
+    print(f"n={n} waves={r.waves} strips={r.strips} kernel_ms={r.kernel_ms:.3f} (untraced {r0.kernel_ms:.3f}) "
+          f"span_us={en.max():.0f}")
+    print(f"  strip duration us: min {dur.min():.0f} med {np.median(dur):.0f} max {dur.max():.0f}"
+          f"  -> per row {np.median(dur)/n*1000:.2f} ns")
+    print(f"  start lag us: med {np.median(lag):.2f} p10 {np.percentile(lag,10):.2f} p90 {np.percentile(lag,90):.2f}")
+    print(f"  slow waits/strip: med {np.median(t[:,2]):.0f} max {t[:,2].max():.0f}; wait us/strip med "
+          f"{np.median(t[:,3])/100:.0f} max {t[:,3].max()/100:.0f}")
+    for q in [0, 1, 2, nstrips // 4, nstrips // 2, nstrips - 2, nstrips - 1]:
+        print(f"   strip {q}: start {st[q]:.1f} end {en[q]:.1f} dur {dur[q]:.1f} slow {t[q,2]:.0f} wait {t[q,3]/100:.1f}")
