@@ -31,12 +31,11 @@ struct nw_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int last_waves = 0;
     int last_strips = 0;
+    int last_sub = 0;
     uint64_t *trace = nullptr;  // debug: per-strip timestamps (nw_debug_set_trace)
 };
 
 namespace {
-
-constexpr int kWavesPerCU = 4;  // 33 KB LDS per single-wave workgroup -> 4 per CU
 
 inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
@@ -64,15 +63,22 @@ int grow(void **p, size_t *cap, size_t need, bool zero) {
 
 struct Shape {
     int64_t nRows, nCols, nstrips, nblocks, waves, M, gstride;
+    int32_t K;
 };
 
-Shape make_shape(int64_t n1, int64_t n2, int32_t waves_req, int cus) {
+constexpr int kDefaultSub = 2;
+constexpr int kLdsPerCU = 160 * 1024;
+
+Shape make_shape(int64_t n1, int64_t n2, int32_t waves_req, int32_t sub_req, int cus) {
     Shape s;
+    s.K = sub_req > 0 ? sub_req : kDefaultSub;
     s.nRows = n2 + 1;
     s.nCols = n1 + 1;
-    s.nstrips = (s.nCols + nw::kWave - 1) / nw::kWave;
+    s.nstrips = (s.nCols + nw::kWave * s.K - 1) / (nw::kWave * s.K);
     s.nblocks = (s.nRows + nw::kWave - 1) / nw::kWave;
-    int64_t w = waves_req > 0 ? waves_req : (int64_t)kWavesPerCU * cus;
+    // one single-wave workgroup per LDS ring set; as many as fit in a CU's LDS
+    const int64_t per_cu = std::max(1, kLdsPerCU / nw::lds_bytes(s.K));
+    int64_t w = waves_req > 0 ? waves_req : per_cu * cus;
     s.waves = std::max<int64_t>(1, std::min<int64_t>(w, s.nstrips));
     // Strip p publishes into slot p % M.  When strip p is claimed, every strip
     // <= p - waves has finished, so M = waves + 1 slots never alias a live one.
@@ -84,6 +90,7 @@ Shape make_shape(int64_t n1, int64_t n2, int32_t waves_req, int cus) {
 bool valid_params(const nw_params *p) {
     if (!p) return false;
     if (p->mode != NW_MODE_NW) return false;
+    if (p->substrips != 0 && p->substrips != 1 && p->substrips != 2 && p->substrips != 4) return false;
     // keep every intermediate far from int32 overflow (|score| < 2^29)
     const int32_t lim = 1 << 12;
     return std::abs(p->match) < lim && std::abs(p->mismatch) < lim && std::abs(p->gap) < lim;
@@ -130,7 +137,7 @@ int64_t nw_table_bytes(int64_t n1, int64_t n2) {
 }
 
 int64_t nw_ctx_workspace_bytes(int64_t n1, int64_t n2, int32_t waves) {
-    Shape s = make_shape(n1, n2, waves, 256);
+    Shape s = make_shape(n1, n2, waves, 0, 256);
     return s.M * s.gstride * 8 + nw::rowpack_len((int32_t)s.nblocks) * 4 +
            s.waves * nw::kScratchWords * 4 + 16;
 }
@@ -183,7 +190,7 @@ int nw_fill_device_async(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t
     if (pitch < nw_table_pitch(n1) || pitch % nw::kWave != 0) return NW_ERR_ARG;
     if (((uintptr_t)d_t & 255u) != 0) return NW_ERR_ARG;
     NW_HIP_TRY(hipSetDevice(c->device));
-    const Shape s = make_shape(n1, n2, p->waves, c->cus);
+    const Shape s = make_shape(n1, n2, p->waves, p->substrips, c->cus);
     if (s.nstrips > INT32_MAX / 2 || s.nblocks > INT32_MAX / 2) return NW_ERR_ARG;
 
     int st;
@@ -232,10 +239,11 @@ int nw_fill_device_async(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t
     a.mismatch = p->mismatch;
     a.gap = p->gap;
     a.flags = p->flags;
-    if (nw::launch_fill(a, (int)s.waves, stream) != hipSuccess) return NW_ERR_HIP;
+    if (nw::launch_fill(a, s.K, (int)s.waves, stream) != hipSuccess) return NW_ERR_HIP;
     c->tagbase += (uint32_t)s.nstrips + 1u;
     c->last_waves = (int)s.waves;
     c->last_strips = (int)s.nstrips;
+    c->last_sub = s.K;
     return NW_OK;
 }
 
@@ -267,6 +275,7 @@ int nw_fill_device(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *d_s2
     out->table_bytes = (double)(n1 + 1) * (double)(n2 + 1) * 4.0;
     out->strips = c->last_strips;
     out->waves = c->last_waves;
+    out->substrips = c->last_sub;
     int32_t score = 0;
     NW_HIP_TRY(hipMemcpy(&score, d_t + n2 * pitch + n1, 4, hipMemcpyDeviceToHost));
     out->score = score;

@@ -7,23 +7,29 @@
 //   t[i][j] = max(t[i-1][j-1] + s(s1[j-1], s2[i-1]), t[i-1][j] + GAP, t[i][j-1] + GAP)
 //   t[0][j] = j*GAP, t[i][0] = i*GAP                              (serial.cpp:16-17)
 //
-// Decomposition:
-//   * The table is cut into vertical STRIPS of 64 columns.  One wave64 owns a
-//     strip: lane l owns column c = 64p + l and sweeps the rows.  At step s lane l
-//     computes row i = s - l (anti-diagonal wavefront inside the wave).
+// Decomposition (DESIGN.md has the full picture):
+//   * The table is cut into vertical SUPER-STRIPS of K*64 columns, one wave64
+//     each, made of K 64-column SUB-STRIPS.  In sub-strip k lane l owns column
+//     c = 64*(K*p + k) + l and at step s computes row i = s - 64k - l: an
+//     anti-diagonal wavefront inside the wave, sub-strip k trailing k-1 by 64
+//     steps.
 //       up   = t[i-1][c]   : the lane's own previous result (register)
-//       left = t[i][c-1]   : lane l-1's previous result, moved by DPP wave_shr:1
+//       left = t[i][c-1]   : lane l-1's previous result, DPP wave_shr:1
 //       diag = t[i-1][c-1] : lane l-1's result two steps back = last step's `left`
-//     Lane 0 takes left/diag from the strip to its left (the "feed").
-//   * Every value is written to a 128-row LDS ring (row-indexed); at the end of
-//     each 64-step iteration the 64 rows that became complete are flushed as
-//     row-contiguous 256-B segments (ds_read_b128 -> global_store_dwordx4).
-//   * Strip-to-strip hand-off: the right column of strip p (lane 63) is
-//     published per 64-row block as 8-byte {tag, value} granules written with
-//     agent-scope atomic stores (the data is the flag; no fences).  Strip p+1
-//     polls them with agent-scope loads.  This is the GPU analogue of
+//     Lane 0 of sub-strip k >= 1 takes left/diag from lane 63 of sub-strip k-1
+//     (DPP wave_ror:1 of the previous step -- an in-register hand-off); lane 0
+//     of sub-strip 0 takes them from the super-strip to the left (the "feed").
+//     The K chains are independent within a step, so they interleave (ILP).
+//   * Every value is written to a 128-row LDS ring per sub-strip (row-indexed);
+//     at the end of each 64-step iteration the 64 rows that became complete are
+//     flushed as row-contiguous 256-B segments (ds_read_b128 ->
+//     global_store_dwordx4, 4 rows per instruction).
+//   * Super-strip to super-strip hand-off: the right column (sub-strip K-1,
+//     lane 63) is published per 64-row block as 8-byte {tag, value} granules
+//     with agent-scope atomic stores (the data is the flag; no fences); the next
+//     super-strip polls them with agent-scope loads -- the GPU analogue of
 //     idxarray-mt's per-row progress counters (idxarray-mt.cpp:8,44,50-56).
-//   * Strips are claimed from an atomic ticket in increasing order by a
+//   * Super-strips are claimed from an atomic ticket in increasing order by a
 //     persistent grid of single-wave workgroups, so a strip's producer is always
 //     already running: deadlock-free for any grid size / residency.
 //   * Pure int32 VALU + LDS + HBM stores; no MFMA (there is no contraction).
@@ -38,8 +44,8 @@ namespace nw {
 
 // s_memrealtime runs at 100 MHz on gfx9: 20 s watchdog for every bounded spin.
 constexpr uint64_t kTimeoutTicks = 100000000ull * 20ull;
-constexpr int kLdsTile = kRing * kWave;          // int32 words of the staging ring
-constexpr int kLdsWords = kLdsTile + kRing;      // + feed ring (left boundary)
+constexpr int kRingWords = kRing * kWave;  // int32 words of one sub-strip's staging ring
+constexpr int kRingBytes = kRingWords * 4;
 
 __device__ __forceinline__ uint64_t gran_load(const uint64_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -56,7 +62,7 @@ __device__ __forceinline__ uint32_t ctrl_load(const uint32_t *p) {
 // kTimeoutTicks, or at once if another wave already raised it.  Returns the last
 // value read; the caller re-checks its tag.
 __device__ __forceinline__ uint64_t wait_granules_slow(const uint64_t *g, uint32_t tag,
-                                                    uint32_t *ctrl) {
+                                                       uint32_t *ctrl) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
         __builtin_amdgcn_s_sleep(1);
@@ -70,11 +76,11 @@ __device__ __forceinline__ uint64_t wait_granules_slow(const uint64_t *g, uint32
     }
 }
 
-// Row characters for the 64 steps of iteration `it`: pack g holds the bytes of
-// rows 64*it + 4g - lane + {0,1,2,3} (one dword per 4 steps per lane).
-__device__ __forceinline__ void load_packs(const uint32_t *__restrict__ q, int it, int lane,
+// Row characters for the 64 steps of local iteration j: pack g holds the bytes
+// of rows 64*j + 4g - lane + {0,1,2,3} (one dword per 4 steps per lane).
+__device__ __forceinline__ void load_packs(const uint32_t *__restrict__ q, int j, int lane,
                                            uint32_t (&pk)[16]) {
-    const uint32_t *base = q + kQOff + (int64_t)it * 64 - lane;
+    const uint32_t *base = q + kQOff + (int64_t)max(j, 0) * 64 - lane;
 #pragma unroll
     for (int g = 0; g < 16; ++g) pk[g] = base[4 * g];
 }
@@ -119,113 +125,184 @@ __device__ __forceinline__ int32_t diag_plus_sub(uint32_t pk, uint32_t a, int32_
     return d;
 }
 
-// 64 wavefront steps of one iteration (rows 64*it + u - lane, u = 0..63).
-// RAMP: first iteration of a strip -- lanes whose row is still <= 0
-// (lane >= u) keep their row-0 state and re-emit t[0][c].
-template <bool RAMP, bool UNIT>
-__device__ __forceinline__ void run_iter(int32_t *__restrict__ lds, int it, int lane,
-                                         const uint32_t (&pk)[16], uint32_t a, int32_t msp,
-                                         int32_t mmp, int32_t gap, int32_t &tg, int32_t &tl_old,
-                                         uint32_t &laddr) {
-    // feed (left strip's t[i][c0-1] + GAP for the 64 rows of this iteration),
-    // read 4 rows per ds_read_b128, one group ahead of use.
-    const int4 *feed4 = (const int4 *)(lds + kLdsTile + ((it & 1) << 6));
+// Per-lane state of one super-strip.
+template <int K>
+struct Lanes {
+    uint32_t a[K];   // column character of this lane in sub-strip k
+    int32_t tg[K];   // t(current row of the lane) + GAP  (up + GAP for the next step)
+    int32_t tl[K];   // last step's left + GAP  (= diag' for this step)
+    int32_t rr[K];   // RAMP: row index of the lane in sub-strip k at the current step
+};
+
+// Sub-strip modes in an iteration: IDLE (not started), RAMP (first iteration,
+// lanes with row <= 0 hold row 0), RUN.
+enum Mode { IDLE = 0, RAMP = 1, RUN = 2 };
+
+template <int IT>
+constexpr int prologue_mode(int k) {
+    return IT - k < 0 ? IDLE : (IT - k == 0 ? RAMP : RUN);
+}
+
+// 64 wavefront steps of one iteration for all K sub-strips.  MODES packs the
+// mode of sub-strip k in bits [2k, 2k+1].  Sub-strips are processed from K-1
+// down to 0 inside a step so that sub-strip k reads sub-strip k-1's register
+// state of the PREVIOUS step.
+template <int K, bool UNIT, int MODES>
+__device__ __forceinline__ void run_iter(int32_t *__restrict__ lds, int it,
+                                         const uint32_t (&pk)[K][16], int32_t msp, int32_t mmp,
+                                         int32_t gap, Lanes<K> &S, uint32_t laddr,
+                                         int32_t *const (&fdst)[K], const int64_t (&fpitch)[K],
+                                         int lane) {
+    // Interleaved flush: the ring half this iteration overwrites holds the block
+    // that completed in the previous iteration.  Before the 4 steps of group g
+    // overwrite its rows 4g..4g+3, those rows are read (ds_read_b128, 4 rows x
+    // 64 columns) and stored (global_store_dwordx4, 4 x 256 B row segments), so
+    // the 16 stores of a block trickle out one per 4 steps instead of in a burst.
+    const int rsub = lane >> 4, csub = (lane & 15) * 4;
+    const int fbase = (((it & 1) << 6) + rsub) * 64 + csub;
+    // feed of sub-strip 0 (left super-strip's t[i][c0-1] + GAP for the 64 rows
+    // of this iteration), read 4 rows per ds_read_b128, one group ahead.
+    const int4 *feed4 = (const int4 *)(lds + K * kRingWords + ((it & 1) << 6));
     int4 fq = feed4[0];
-    int32_t rr = -lane - 1;  // RAMP: row index of this lane at the current step (opaque)
+    // keep the 64 per-step ring offsets in-loop (2 VALU/step shared by all K
+    // sub-strips) instead of letting hipcc hoist 64 address VGPRs
+    asm volatile("" : "+v"(laddr));
     static_for<0, 16>([&](auto gc) {
         constexpr int g = decltype(gc)::value;
         const int4 fcur = fq;
         if constexpr (g + 1 < 16) fq = feed4[g + 1];
-        static_for<0, 4>([&](auto kc) {
-            constexpr int k = decltype(kc)::value;
-            constexpr int u = 4 * g + k;
-            const int32_t fv = k == 0 ? fcur.x : k == 1 ? fcur.y : k == 2 ? fcur.z : fcur.w;
-            // left + GAP: lane l-1's last result; lane 0 gets the left strip's value.
-            const int32_t tl_new = __builtin_amdgcn_update_dpp(fv, tg, 0x138 /*wave_shr:1*/,
-                                                               0xF, 0xF, false);
-            const int32_t d = diag_plus_sub<k, UNIT>(pk[g], a, tl_old, msp, mmp);
-            int32_t t = max(max(d, tg), tl_new);  // max(diag+s, up+GAP, left+GAP)
-            if constexpr (RAMP) {
-                rr += 1;
-                asm volatile("" : "+v"(rr));  // keep the per-step activity test in the loop
-                const int32_t tgn = (rr >= 1) ? t + gap : tg;
-                t = tgn - gap;
-                tg = tgn;
-            } else {
-                tg = t + gap;
-            }
-            tl_old = tl_new;
-            laddr = (laddr + 256u) & 0x7FFFu;  // ring row (i & 127) * 256 B + 4*lane
-            *(int32_t *)((char *)lds + laddr) = t;
-            (void)u;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int4 v = *(const int4 *)(lds + k * kRingWords + fbase + g * 256);
+            *(int4 *)(fdst[k] + (int64_t)(4 * g + rsub) * fpitch[k] + csub) = v;
+        }
+        static_for<0, 4>([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            constexpr int u = 4 * g + q;
+            const uint32_t off = (laddr + 256u * (uint32_t)(u + 1)) & 0x7FFFu;  // ring row (i & 127)
+            static_for<0, K>([&](auto kk) {
+                constexpr int k = K - 1 - decltype(kk)::value;  // K-1 .. 0
+                constexpr int mode = (MODES >> (2 * k)) & 3;
+                if constexpr (mode != IDLE) {
+                    int32_t lf;  // lane-0 source of `left`
+                    if constexpr (k == 0) {
+                        lf = q == 0 ? fcur.x : q == 1 ? fcur.y : q == 2 ? fcur.z : fcur.w;
+                    } else {
+                        // lane 0 <- lane 63 of sub-strip k-1, previous step (wave_ror:1)
+                        lf = __builtin_amdgcn_update_dpp(0, S.tg[k - 1], 0x13C, 0xF, 0xF, false);
+                    }
+                    const int32_t tl_new = __builtin_amdgcn_update_dpp(lf, S.tg[k], 0x138 /*wave_shr:1*/,
+                                                                       0xF, 0xF, false);
+                    const int32_t d = diag_plus_sub<q, UNIT>(pk[k][g], S.a[k], S.tl[k], msp, mmp);
+                    int32_t t = max(max(d, S.tg[k]), tl_new);  // max(diag+s, up+GAP, left+GAP)
+                    if constexpr (mode == RAMP) {
+                        S.rr[k] += 1;
+                        asm volatile("" : "+v"(S.rr[k]));  // keep the activity test in the loop
+                        const int32_t tgn = (S.rr[k] >= 1) ? t + gap : S.tg[k];
+                        t = tgn - gap;
+                        S.tg[k] = tgn;
+                    } else {
+                        S.tg[k] = t + gap;
+                    }
+                    S.tl[k] = tl_new;
+                    *(int32_t *)((char *)lds + k * kRingBytes + off) = t;
+                }
+            });
         });
     });
 }
 
-// Flush block fb (64 rows that became complete) of strip p from the LDS ring to
-// HBM as row-contiguous segments: each ds_read_b128 / global_store_dwordx4 pair
-// moves 4 rows x 256 B.  The device table holds round_up(nRows, 64) rows, so the
-// rows past n2 of the last block land in padding and no store is masked.  Then
-// publish the strip's right column (lane 63's values) for rows of this block as
-// {tag, value} granules for strip p+1 (the last strip publishes into its own,
-// never-read slot: keeps the store count branch-free).
-__device__ __forceinline__ void flush_block(const int32_t *__restrict__ lds, int fb, int lane,
-                                            int32_t *dst, int64_t pitch, uint64_t *gout,
-                                            uint32_t tag_out) {
-    const int sbase = (fb & 1) << 6;
+// Flush one 64-row block of one sub-strip from its LDS ring to `dst` (row-major,
+// `pitch` int32) as row-contiguous segments: each ds_read_b128 /
+// global_store_dwordx4 pair moves 4 rows x 256 B.  `sbase` = ring row of the
+// block's first row (0 or 64).
+__device__ __forceinline__ void flush_rows(const int32_t *__restrict__ ring, int sbase, int lane,
+                                           int32_t *dst, int64_t pitch) {
     const int rsub = lane >> 4, csub = (lane & 15) * 4;
     int32_t *g = dst + rsub * pitch + csub;
-    const int4 *src = (const int4 *)(lds + (sbase + rsub) * 64 + csub);
+    const int4 *src = (const int4 *)(ring + (sbase + rsub) * 64 + csub);
     const int64_t step4 = 4 * pitch;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
         const int4 v = src[q * 64];  // 4 rows down = 4*64 words = 64 int4
         *(int4 *)(g + q * step4) = v;
     }
-    const int32_t v = lds[(sbase + lane) * 64 + 63];
-    gran_store(gout + lane, ((uint64_t)tag_out << 32) | (uint32_t)v);
 }
 
-template <bool UNIT>
+template <int K, bool UNIT>
 __device__ void process_strip(const FillArgs &A, int32_t *__restrict__ lds, int p, int lane) {
-    const int64_t c = (int64_t)p * 64 + lane;
     const int32_t gap = A.gap;
     const int32_t msp = A.match - gap, mmp = A.mismatch - gap;
-    const uint32_t a = (c >= 1 && c <= A.n1) ? (uint32_t)A.s1[c - 1] : 0u;
-    int32_t top = (int32_t)(c * (int64_t)gap);
-    if (A.top != nullptr && c <= A.n1) top = A.top[c];
-    int32_t tg = top + gap;  // t[0][c] + GAP
-    int32_t tl_old = 0;
-    uint32_t laddr = ((uint32_t)(-1 - lane) & 127u) * 256u + (uint32_t)lane * 4u;
+    const int64_t c0 = (int64_t)p * (64 * K);
+    Lanes<K> S;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int64_t c = c0 + 64 * k + lane;
+        S.a[k] = (c >= 1 && c <= A.n1) ? (uint32_t)A.s1[c - 1] : 0u;
+        int32_t top = (int32_t)(c * (int64_t)gap);
+        if (A.top != nullptr && c <= A.n1) top = A.top[c];
+        S.tg[k] = top + gap;  // t[0][c] + GAP
+        S.tl[k] = 0;
+        S.rr[k] = -lane - 1;
+    }
+    // ring byte offset of this lane before step 0 of an even iteration: ring row
+    // (s - lane) & 127 at step s (every sub-strip: sub-strip k stores row i at
+    // ring row (i + 64k) & 127), + 4 * lane
+    const uint32_t lbase = ((uint32_t)(-1 - lane) & 127u) * 256u + (uint32_t)lane * 4u;
 
     const bool has_left = p > 0;
     const uint64_t *gin = A.gran + (int64_t)((p + A.M - 1) % A.M) * A.gstride + lane;
     uint64_t *gout = A.gran + (int64_t)(p % A.M) * A.gstride;
     const uint32_t tag_in = A.tagbase + (uint32_t)p;
     const uint32_t tag_out = A.tagbase + (uint32_t)p + 1u;
+    const int lastb = A.nblocks - 1;
+    int32_t *scr = A.scratch + (int64_t)blockIdx.x * kScratchWords;
+    bool valid[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) valid[k] = c0 + 64 * k < A.pitch;
 
     // Prefetch pipeline (all loads unconditional, so no loop-carried register
-    // copies force an early s_waitcnt that would drain the flush stores):
-    //   granules of block it+1 and row packs of iteration it+1 are issued at the
-    //   start of iteration it, before that iteration's flush stores.
-    const int lastb = A.nblocks - 1;
-    uint64_t gv = gran_load(gin);  // block 0 (slot of strip p-1; unused when p == 0)
-    uint32_t pkA[16], pkB[16];
-    load_packs(A.rowpack, 0, lane, pkA);
+    // copies force an early s_waitcnt that would drain the flush stores): the
+    // granules and row packs used by later iterations are issued at the start of
+    // iteration it, before that iteration's flush stores.
+    // Prefetch pipeline.  Everything an iteration reads from global memory (the
+    // left neighbour's granules for its feed, the row-character packs of its K
+    // sub-strips) is loaded TWO iterations ahead into 3-deep register rings:
+    // under full store traffic a load queues behind this CU's stores for longer
+    // than an iteration, and vmcnt is in-order, so a load consumed one iteration
+    // later would stall the wave every iteration.  Buffer = issue iteration mod 3;
+    // iteration i consumes buffer (i+1) % 3 and refills buffer i % 3.  All loads
+    // are unconditional (clamped indices) so every path carries the same VMEM
+    // count for hipcc's s_waitcnt bookkeeping.
+    uint64_t gb[3];
+    uint32_t pkb[3][K][16];
+    gb[1] = gran_load(gin);                                  // block 0, for iteration 0
+    gb[2] = gran_load(gin + (int64_t)min(1, lastb) * 64);    // block 1, for iteration 1
+    gb[0] = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        load_packs(A.rowpack, 0 - k, lane, pkb[1][k]);
+        load_packs(A.rowpack, 1 - k, lane, pkb[2][k]);
+    }
 
-    // One iteration: feed for block it, prefetch it+1, 64 steps, flush block it-1.
-    // A watchdog trip only marks the strip dead; the iteration still issues the
-    // same VMEM operations so every path into the next iteration is identical for
-    // hipcc's s_waitcnt accounting, and the strip is abandoned at the boundary.
     bool dead = false;
     uint32_t nslow = 0;
     uint64_t wticks = 0;
     const uint64_t tstart = __builtin_amdgcn_s_memrealtime();
-    auto iter = [&](int it, const uint32_t(&pk)[16], uint32_t(&pkn)[16], auto ramp) {
-        constexpr bool RAMP = decltype(ramp)::value;  // first iteration: no block to flush yet
+
+    // One iteration: feed for block it, prefetch for it+2, flush (interleaved
+    // with the steps), 64 steps.  A watchdog trip only marks the strip dead; the
+    // iteration still issues the same VMEM operations, so every path into the next
+    // iteration is identical for s_waitcnt accounting, and the strip is abandoned
+    // at the boundary.
+    auto iter = [&](int it, auto cons_c, auto iss_c, auto modes) {
+        constexpr int CONS = decltype(cons_c)::value;  // (it + 1) % 3
+        constexpr int ISS = decltype(iss_c)::value;    // it % 3
+        constexpr int MODES = decltype(modes)::value;
         if (it < A.nblocks) {
             int32_t fvv = kNeg;
             if (has_left) {
+                uint64_t gv = gb[CONS];  // block it, loaded two iterations ago
                 if (!__all((uint32_t)(gv >> 32) == tag_in)) {
                     const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
                     gv = wait_granules_slow(gin + (int64_t)it * 64, tag_in, A.ctrl);
@@ -235,36 +312,65 @@ __device__ void process_strip(const FillArgs &A, int32_t *__restrict__ lds, int 
                 }
                 fvv = (int32_t)(uint32_t)gv + gap;
             }
-            lds[kLdsTile + ((it & 1) << 6) + lane] = fvv;
+            lds[K * kRingWords + ((it & 1) << 6) + lane] = fvv;
         }
-        gv = gran_load(gin + (int64_t)min(it + 1, lastb) * 64);
-        load_packs(A.rowpack, it + 1, lane, pkn);
-        run_iter<RAMP, UNIT>(lds, it, lane, pk, a, msp, mmp, gap, tg, tl_old, laddr);
-        if constexpr (!RAMP) {
-            const int64_t row0 = (int64_t)(it - 1) * 64;
-            int32_t *dst = A.table + row0 * A.pitch + (int64_t)p * 64;
-            int64_t pitch = A.pitch;
-            if (A.flags & 1) {  // debug timing mode: keep the stores, drop the HBM traffic
-                dst = A.scratch + (int64_t)blockIdx.x * kScratchWords;
-                pitch = kWave;
-            }
-            flush_block(lds, it - 1, lane, dst, pitch, gout + row0, tag_out);
-        } else {
-            // Nothing is complete yet.  Issue the same 17 stores into this
-            // workgroup's scratch tile so that every path into the steady-state
-            // loop carries the same VMEM count (hipcc's s_waitcnt bookkeeping then
-            // never has to drain the previous flush to read the row packs).
-            int32_t *scr = A.scratch + (int64_t)blockIdx.x * kScratchWords;
-            flush_block(lds, 1, lane, scr, kWave, (uint64_t *)(scr + kWave * kWave), 0u);
+        gb[ISS] = gran_load(gin + (int64_t)min(it + 2, lastb) * 64);
+#pragma unroll
+        for (int k = 0; k < K; ++k) load_packs(A.rowpack, it + 2 - k, lane, pkb[ISS][k]);
+        // Flush what completed in the PREVIOUS iteration (sub-strip k: block
+        // it-2-k), interleaved with this iteration's steps (see run_iter).  The
+        // prefetch loads above are issued first: vmcnt is in-order, so a load
+        // waited for later never queues behind these stores.  Blocks outside the
+        // table (not yet started / past the end / columns past the pitch) go to
+        // this workgroup's scratch tile, so every iteration issues the same
+        // K*16 + 1 stores.
+        int32_t *fdst[K];
+        int64_t fpitch[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int b = it - 2 - k;
+            const bool ok = valid[k] && b >= 0 && b < A.nblocks && !(A.flags & 1);
+            fdst[k] = ok ? A.table + (int64_t)b * 64 * A.pitch + c0 + 64 * k : scr;
+            fpitch[k] = ok ? A.pitch : (int64_t)kWave;
         }
+        {
+            // right column of the super-strip (sub-strip K-1, lane 63) for block b,
+            // read before this iteration's steps overwrite the ring half
+            const int sbase = (it & 1) << 6;
+            const int b = it - 1 - K;
+            const int32_t v = lds[(K - 1) * kRingWords + (sbase + lane) * 64 + 63];
+            const bool ok = b >= 0 && b < A.nblocks;
+            uint64_t *gp = ok ? gout + (int64_t)b * 64 + lane
+                              : (uint64_t *)(scr + kWave * kWave) + lane;
+            gran_store(gp, ((uint64_t)tag_out << 32) | (uint32_t)v);
+        }
+        run_iter<K, UNIT, MODES>(lds, it, pkb[CONS], msp, mmp, gap, S,
+                                 lbase + (uint32_t)(it & 1) * (64u * 256u), fdst, fpitch, lane);
     };
 
-    const int nit = A.nblocks + 1;  // iteration nblocks completes the last block
-    iter(0, pkA, pkB, std::true_type{});
-    for (int it = 1; it < nit && !dead; it += 2) {
-        iter(it, pkB, pkA, std::false_type{});
+    // sub-strip K-1 completes the last block in iteration nblocks-1+K; it is
+    // flushed at the start of the next one (whose 64 steps are wasted work)
+    const int nit = A.nblocks + K + 1;
+    // prologue iterations 0..K-1 (sub-strips start one after another)
+    static_for<0, K>([&](auto itc) {
+        constexpr int IT = decltype(itc)::value;
+        constexpr int MODES = (prologue_mode<IT>(0) | (prologue_mode<IT>(1) << 2) |
+                               (prologue_mode<IT>(2) << 4) | (prologue_mode<IT>(3) << 6)) &
+                              ((1 << (2 * K)) - 1);
+        iter(IT, std::integral_constant<int, (IT + 1) % 3>{}, std::integral_constant<int, IT % 3>{},
+             std::integral_constant<int, MODES>{});
+    });
+    constexpr int RUNALL = (RUN | (RUN << 2) | (RUN << 4) | (RUN << 6)) & ((1 << (2 * K)) - 1);
+    constexpr int P0 = K % 3;  // ring phase of the first steady iteration
+    for (int it = K; it < nit && !dead; it += 3) {
+        iter(it, std::integral_constant<int, (P0 + 1) % 3>{}, std::integral_constant<int, P0>{},
+             std::integral_constant<int, RUNALL>{});
         if (it + 1 >= nit || dead) break;
-        iter(it + 1, pkA, pkB, std::false_type{});
+        iter(it + 1, std::integral_constant<int, (P0 + 2) % 3>{},
+             std::integral_constant<int, (P0 + 1) % 3>{}, std::integral_constant<int, RUNALL>{});
+        if (it + 2 >= nit || dead) break;
+        iter(it + 2, std::integral_constant<int, (P0 + 3) % 3>{},
+             std::integral_constant<int, (P0 + 2) % 3>{}, std::integral_constant<int, RUNALL>{});
     }
     if (A.trace != nullptr && lane == 0) {
         uint64_t *tr = A.trace + (int64_t)p * 4;
@@ -275,16 +381,16 @@ __device__ void process_strip(const FillArgs &A, int32_t *__restrict__ lds, int 
     }
 }
 
-template <bool UNIT>
+template <int K, bool UNIT>
 __global__ __launch_bounds__(64) void nw_fill_strips(FillArgs A) {
-    __shared__ __attribute__((aligned(16))) int32_t lds[kLdsWords];
+    __shared__ __attribute__((aligned(16))) int32_t lds[K * kRingWords + kRing];
     const int lane = threadIdx.x;
     for (;;) {
         uint32_t p = 0;
         if (lane == 0) p = atomicAdd(A.ctrl, 1u);
         p = __builtin_amdgcn_readfirstlane(p);
         if (p >= (uint32_t)A.nstrips) break;
-        process_strip<UNIT>(A, lds, (int)p, lane);
+        process_strip<K, UNIT>(A, lds, (int)p, lane);
     }
 }
 
@@ -305,7 +411,7 @@ __global__ void nw_rowpack(const uint8_t *__restrict__ s2, int64_t n2, int64_t r
     q[idx] = v;
 }
 
-int64_t rowpack_len(int32_t nblocks) { return kQOff + 64 * ((int64_t)nblocks + 2) + 8; }
+int64_t rowpack_len(int32_t nblocks) { return kQOff + 64 * ((int64_t)nblocks + kMaxSub + 2) + 8; }
 
 int launch_rowpack(const uint8_t *d_s2, int64_t n2, int64_t row0, uint32_t *d_q, int64_t qlen,
                    void *stream) {
@@ -316,14 +422,27 @@ int launch_rowpack(const uint8_t *d_s2, int64_t n2, int64_t row0, uint32_t *d_q,
     return (int)hipGetLastError();
 }
 
-int launch_fill(const FillArgs &a, int grid, void *stream) {
+template <int K>
+static void launch_k(const FillArgs &a, int grid, hipStream_t s) {
     if (a.match - a.mismatch == 1)
-        hipLaunchKernelGGL(nw_fill_strips<true>, dim3(grid), dim3(kWave), 0, (hipStream_t)stream, a);
+        hipLaunchKernelGGL((nw_fill_strips<K, true>), dim3(grid), dim3(kWave), 0, s, a);
     else
-        hipLaunchKernelGGL(nw_fill_strips<false>, dim3(grid), dim3(kWave), 0, (hipStream_t)stream, a);
+        hipLaunchKernelGGL((nw_fill_strips<K, false>), dim3(grid), dim3(kWave), 0, s, a);
+}
+
+int launch_fill(const FillArgs &a, int substrips, int grid, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    switch (substrips) {
+        case 1: launch_k<1>(a, grid, s); break;
+        case 2: launch_k<2>(a, grid, s); break;
+        case 4: launch_k<4>(a, grid, s); break;
+        default: return (int)hipErrorInvalidValue;
+    }
     return (int)hipGetLastError();
 }
 
-const char *kernel_variant() { return "strip64-dpp-ldsring128-gran64"; }
+int lds_bytes(int substrips) { return (substrips * kRingWords + kRing) * 4; }
+
+const char *kernel_variant() { return "superstrip-Kx64-dpp-ldsring128-gran64"; }
 
 }  // namespace nw

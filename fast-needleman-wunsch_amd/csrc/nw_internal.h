@@ -10,6 +10,7 @@ constexpr int kRing = 128;         // rows held by the LDS staging ring (2 block
 constexpr int kQOff = 64;          // rowpack index offset (lane l reads index 4g - l)
 constexpr int32_t kNeg = -(1 << 29);  // "minus infinity" fed left of column 0
 constexpr int kScratchWords = kWave * kWave + 2 * kWave;  // per workgroup (16.5 KB)
+constexpr int kMaxSub = 4;        // max 64-column sub-strips per wave (LDS: 32 KB each)
 
 // Everything one launch of the strip-sweep kernel needs.  Plain POD, passed by
 // value as the kernel argument.
@@ -21,7 +22,7 @@ struct FillArgs {
     const uint8_t *s1;         // n1 column characters
     int64_t n1, n2;            // nCols = n1 + 1, nRows = n2 + 1
     int64_t row0;              // global row index of local row 0 (0 for a whole table)
-    int32_t nstrips;           // ceil(nCols / 64)
+    int32_t nstrips;           // super-strips: ceil(nCols / (64 * substrips))
     int32_t nblocks;           // ceil(nRows / 64)
     uint64_t *gran;            // right-boundary hand-off granules [M][gstride] {tag:32 | value:32}
     int64_t gstride;           // granules per slot = 64 * nblocks
@@ -38,7 +39,8 @@ struct FillArgs {
 // Launch helpers implemented in nw_fill.hip.  Return hipError_t as int.
 int launch_rowpack(const uint8_t *d_s2, int64_t n2, int64_t row0, uint32_t *d_q, int64_t qlen,
                    void *stream);
-int launch_fill(const FillArgs &a, int grid, void *stream);
+int launch_fill(const FillArgs &a, int substrips, int grid, void *stream);
+int lds_bytes(int substrips);
 int64_t rowpack_len(int32_t nblocks);
 const char *kernel_variant();
 

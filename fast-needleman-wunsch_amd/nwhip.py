@@ -32,13 +32,14 @@ EXPORTS = ["nw_params_default", "nw_strerror", "nw_version", "nw_fill", "nw_tabl
 class NwParams(ctypes.Structure):
     _fields_ = [("match", ctypes.c_int32), ("mismatch", ctypes.c_int32), ("gap", ctypes.c_int32),
                 ("mode", ctypes.c_int32), ("waves", ctypes.c_int32), ("device", ctypes.c_int32),
-                ("flags", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("flags", ctypes.c_int32), ("substrips", ctypes.c_int32)]
 
 
 class NwResult(ctypes.Structure):
     _fields_ = [("score", ctypes.c_int32), ("status", ctypes.c_int32), ("cells", ctypes.c_int64),
                 ("kernel_ms", ctypes.c_double), ("table_bytes", ctypes.c_double),
-                ("strips", ctypes.c_int32), ("waves", ctypes.c_int32)]
+                ("strips", ctypes.c_int32), ("waves", ctypes.c_int32),
+                ("substrips", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 class NwError(RuntimeError):
@@ -118,7 +119,8 @@ class Scheme:
     gap: int = -1
 
 
-def params(scheme=(1, 0, -1), waves: int = 0, device: int = -1, flags: int = 0) -> NwParams:
+def params(scheme=(1, 0, -1), waves: int = 0, device: int = -1, flags: int = 0,
+           substrips: int = 0) -> NwParams:
     if isinstance(scheme, Scheme):
         scheme = (scheme.match, scheme.mismatch, scheme.gap)
     p = NwParams()
@@ -127,6 +129,7 @@ def params(scheme=(1, 0, -1), waves: int = 0, device: int = -1, flags: int = 0) 
     p.waves = int(waves)
     p.device = int(device)
     p.flags = int(flags)
+    p.substrips = int(substrips)
     return p
 
 
@@ -136,12 +139,12 @@ def _seq(s) -> np.ndarray:
     return np.ascontiguousarray(np.asarray(s, dtype=np.int8))
 
 
-def fill(s1, s2, scheme=(1, 0, -1), waves: int = 0, device: int = -1):
+def fill(s1, s2, scheme=(1, 0, -1), waves: int = 0, device: int = -1, substrips: int = 0):
     """Full table in the reference layout ((n2+1) x (n1+1) int32) + NwResult."""
     a, b = _seq(s1), _seq(s2)
     t = np.empty((b.size + 1, a.size + 1), dtype=np.int32)
     r = NwResult()
-    p = params(scheme, waves, device)
+    p = params(scheme, waves, device, substrips=substrips)
     st = lib().nw_fill(a.ctypes.data_as(_i8p), a.size, b.ctypes.data_as(_i8p), b.size,
                        ctypes.byref(p), t.ctypes.data_as(_i32p), ctypes.byref(r))
     if st != NW_OK:
@@ -149,10 +152,10 @@ def fill(s1, s2, scheme=(1, 0, -1), waves: int = 0, device: int = -1):
     return t, r
 
 
-def score(s1, s2, scheme=(1, 0, -1), waves: int = 0, device: int = -1) -> int:
+def score(s1, s2, scheme=(1, 0, -1), waves: int = 0, device: int = -1, substrips: int = 0) -> int:
     a, b = _seq(s1), _seq(s2)
     r = NwResult()
-    p = params(scheme, waves, device)
+    p = params(scheme, waves, device, substrips=substrips)
     st = lib().nw_fill(a.ctypes.data_as(_i8p), a.size, b.ctypes.data_as(_i8p), b.size,
                        ctypes.byref(p), None, ctypes.byref(r))
     if st != NW_OK:
@@ -213,7 +216,7 @@ class Context:
         return torch.empty((table_rows(n2), table_pitch(n1)), dtype=torch.int32, device=device)
 
     def fill(self, d_s1, d_s2, table, scheme=(1, 0, -1), waves: int = 0, stream=None,
-             sync: bool = True, flags: int = 0):
+             sync: bool = True, flags: int = 0, substrips: int = 0):
         """d_s1/d_s2: int8/uint8 CUDA tensors; table: from alloc_table.  Returns NwResult
         when sync, else None (launch only)."""
         import torch
@@ -223,7 +226,7 @@ class Context:
         if stream is None:
             stream = torch.cuda.current_stream(table.device)
         sp = ctypes.c_void_p(stream.cuda_stream)
-        p = params(scheme, waves, self.device, flags)
+        p = params(scheme, waves, self.device, flags, substrips)
         args = (self._h, ctypes.c_void_p(d_s1.data_ptr() if n1 else 0), n1,
                 ctypes.c_void_p(d_s2.data_ptr() if n2 else 0), n2, ctypes.byref(p),
                 ctypes.c_void_p(table.data_ptr()), table.shape[1], sp)

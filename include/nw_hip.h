@@ -50,10 +50,10 @@ typedef struct nw_params {
     int32_t mismatch;  /* default  0 */
     int32_t gap;       /* default -1 */
     int32_t mode;      /* NW_MODE_NW */
-    int32_t waves;     /* persistent strip workers (0 = auto)            */
+    int32_t waves;     /* persistent strip workers (waves; 0 = auto)     */
     int32_t device;    /* HIP device ordinal, -1 = current device         */
     int32_t flags;     /* reserved, 0                                     */
-    int32_t reserved;
+    int32_t substrips; /* 64-column sub-strips per wave (1, 2 or 4); 0 = auto */
 } nw_params;
 
 typedef struct nw_result {
@@ -62,8 +62,10 @@ typedef struct nw_result {
     int64_t cells;          /* n1 * n2 inner cells (GCUPS numerator)      */
     double kernel_ms;       /* device time of the fill (HIP events)       */
     double table_bytes;     /* bytes of table stored: 4 * nRows * nCols   */
-    int32_t strips;         /* 64-column strips swept                     */
+    int32_t strips;         /* super-strips swept (substrips*64 columns)  */
     int32_t waves;          /* persistent workers launched                */
+    int32_t substrips;      /* 64-column sub-strips per wave              */
+    int32_t reserved;
 } nw_result;
 
 /* Fill `p` with the reference defaults (1, 0, -1). */

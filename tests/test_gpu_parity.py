@@ -34,11 +34,11 @@ def ctx(torch):
     c.close()
 
 
-def device_fill(torch, ctx, s1, s2, scheme=(1, 0, -1), waves=0):
+def device_fill(torch, ctx, s1, s2, scheme=(1, 0, -1), waves=0, substrips=0):
     d1 = torch.from_numpy(np.ascontiguousarray(s1)).cuda()
     d2 = torch.from_numpy(np.ascontiguousarray(s2)).cuda()
     tab = nwhip.Context.alloc_table(s1.size, s2.size)
-    r = ctx.fill(d1, d2, tab, scheme, waves=waves)
+    r = ctx.fill(d1, d2, tab, scheme, waves=waves, substrips=substrips)
     assert r.status == 0
     return tab, r
 
@@ -95,14 +95,17 @@ SHAPES = [(0, 0), (0, 1), (1, 0), (1, 1), (2, 3), (63, 63), (64, 64), (65, 65), 
 
 @pytest.mark.parametrize("shape", SHAPES)
 @pytest.mark.parametrize("alphabet", ["dna", "bytes"])
-def test_random_vs_oracle(shape, alphabet):
+@pytest.mark.parametrize("substrips", [1, 2, 4])
+def test_random_vs_oracle(shape, alphabet, substrips):
     rng = np.random.default_rng(shape[0] * 7919 + shape[1] + (alphabet == "bytes"))
     lo, hi = (1, 5) if alphabet == "dna" else (-128, 128)
     s1 = rng.integers(lo, hi, shape[0]).astype(np.int8)
     s2 = rng.integers(lo, hi, shape[1]).astype(np.int8)
     for scheme in SCHEMES.values():
-        t, _ = nwhip.fill(s1, s2, scheme)
-        np.testing.assert_array_equal(t, oracle.fill(s1, s2, scheme), err_msg=str((shape, scheme)))
+        t, r = nwhip.fill(s1, s2, scheme, substrips=substrips)
+        assert r.substrips == substrips
+        np.testing.assert_array_equal(t, oracle.fill(s1, s2, scheme),
+                                      err_msg=str((shape, scheme, substrips)))
 
 
 @pytest.mark.parametrize("scheme", [(3, -2, -2), (1, 1, -1), (0, -1, -3), (5, 0, 0), (2, -3, 1)])
@@ -116,14 +119,15 @@ def test_other_schemes_vs_oracle(scheme):
 
 
 @pytest.mark.parametrize("waves", [1, 2, 3, 5, 8, 17, 64])
-def test_worker_count_independent(torch, ctx, waves):
+@pytest.mark.parametrize("substrips", [1, 2, 4])
+def test_worker_count_independent(torch, ctx, waves, substrips):
     """Few persistent workers -> many strips per worker and hand-off slot reuse
     (slot = strip % (waves + 1)); results must not depend on it."""
     rng = np.random.default_rng(waves)
     s1 = rng.integers(1, 5, 64 * 40 + 17).astype(np.int8)
     s2 = rng.integers(1, 5, 900).astype(np.int8)
     want = oracle.fill(s1, s2, (1, -1, -1))
-    tab, r = device_fill(torch, ctx, s1, s2, (1, -1, -1), waves=waves)
+    tab, r = device_fill(torch, ctx, s1, s2, (1, -1, -1), waves=waves, substrips=substrips)
     np.testing.assert_array_equal(tab[:s2.size + 1, :s1.size + 1].cpu().numpy(), want)
     assert r.waves == min(waves, r.strips)
 
@@ -140,12 +144,13 @@ def test_repeated_launches_and_shapes(torch, ctx):
         np.testing.assert_array_equal(tab[:n2 + 1, :n1 + 1].cpu().numpy(), oracle.fill(s1, s2))
 
 
-def test_config2_32k_vs_oracle(torch, ctx):
+@pytest.mark.parametrize("substrips", [1, 2, 4])
+def test_config2_32k_vs_oracle(torch, ctx, substrips):
     """BASELINE config 2: 32k x 32k synthetic (seeds 1, 2), full table in HBM;
     every row checked through (sum, weighted sum), last row/column exactly."""
     n = 32768
     s1, s2 = nwhip.synth(1, n), nwhip.synth(2, n)
-    tab, r = device_fill(torch, ctx, s1, s2, (1, 0, -1))
+    tab, r = device_fill(torch, ctx, s1, s2, (1, 0, -1), substrips=substrips)
     sc, lr, lc, rs, rw = oracle.score(s1, s2, (1, 0, -1), want_rows=True)
     assert r.score == sc
     np.testing.assert_array_equal(tab[n, :n + 1].cpu().numpy(), lr)

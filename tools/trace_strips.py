@@ -14,6 +14,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=32768)
 ap.add_argument("--waves", default="0")
 ap.add_argument("--flags", type=int, default=0)
+ap.add_argument("--sub", type=int, default=0)
 args = ap.parse_args()
 ctx = nwhip.Context(0)
 n = args.n
@@ -24,17 +25,21 @@ nstrips = (n + 1 + 63) // 64
 tr = torch.zeros(nstrips * 4, dtype=torch.int64, device="cuda")
 for w in [int(x) for x in args.waves.split(",")]:
     ctx.set_trace(None)
-    r0 = ctx.fill(s1, s2, tab, waves=w, flags=args.flags)
+    r0 = ctx.fill(s1, s2, tab, waves=w, flags=args.flags, substrips=args.sub)
     ctx.set_trace(tr)
-    r = ctx.fill(s1, s2, tab, waves=w, flags=args.flags)
+    r = ctx.fill(s1, s2, tab, waves=w, flags=args.flags, substrips=args.sub)
+    nstrips = r.strips
     ctx.set_trace(None)
-    t = tr.view(nstrips, 4).cpu().numpy().astype(np.float64)
+    t = tr[: nstrips * 4].view(nstrips, 4).cpu().numpy().astype(np.float64)
     t0 = t[:, 0].min()
     st = (t[:, 0] - t0) / 100.0   # us
     en = (t[:, 1] - t0) / 100.0
     dur = en - st
     lag = np.diff(st)
-    print(f"n={n} waves={r.waves} strips={r.strips} kernel_ms={r.kernel_ms:.3f} (untraced {r0.kernel_ms:.3f}) "
+    busy = (dur - t[:, 3] / 100.0).sum()
+    print(f"  sum(strip time - wait) / (waves * span) = {busy / (r.waves * en.max()):.3f}; "
+          f"sum(wait) / (waves*span) = {t[:, 3].sum() / 100.0 / (r.waves * en.max()):.3f}")
+    print(f"n={n} K={r.substrips} waves={r.waves} strips={r.strips} kernel_ms={r.kernel_ms:.3f} (untraced {r0.kernel_ms:.3f}) "
           f"span_us={en.max():.0f}")
     print(f"  strip duration us: min {dur.min():.0f} med {np.median(dur):.0f} max {dur.max():.0f}"
           f"  -> per row {np.median(dur)/n*1000:.2f} ns")
