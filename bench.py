@@ -6,7 +6,9 @@ A "step" is one complete fill of the table (device-resident: sequences and
 table in HBM before the timed region; nothing copied back inside it).
 
   N = 1 : BASELINE config 3 -- 262144 x 262144 int32 table (275 GB) on one GPU.
-  N > 1 : row-band partition across ranks (mpi-horz contract); see DESIGN.md.
+  N > 1 : row bands across ranks (mpi-horz contract), n1 = 524288 columns and
+          65536 rows per GPU (weak scaling; N = 8 is BASELINE config 4, 512k x 512k);
+          fast-needleman-wunsch_amd/nw_bands.py, DESIGN.md "Multi-GPU".
 
 Prints ONE JSON line on rank 0 (see README / DESIGN.md for field meanings).
 """
@@ -33,6 +35,12 @@ def parse():
     ap.add_argument("--n", type=int, default=262144, help="sequence length (N x N table)")
     ap.add_argument("--scheme", default="1,0,-1", help="match,mismatch,gap")
     ap.add_argument("--waves", type=int, default=0)
+    ap.add_argument("--substrips", type=int, default=0, help="64-col sub-strips per wave (0 = auto)")
+    ap.add_argument("--band-rows", type=int, default=65536,
+                    help="N>1: rows per GPU band (weak scaling; N=8 -> 512k x 512k, config 4)")
+    ap.add_argument("--band-cols", type=int, default=524288, help="N>1: table columns n1")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="N>1 rehearsal: every rank on device 0 (co-resident halves)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-n", type=int, default=65536, help="CPU baseline sample side")
     return ap.parse_args()
@@ -109,7 +117,7 @@ def run_single(args):
     stream = torch.cuda.current_stream()
 
     for _ in range(args.warmup):
-        ctx.fill(s1, s2, tab, scheme, waves=args.waves, sync=False)
+        ctx.fill(s1, s2, tab, scheme, waves=args.waves, sync=False, substrips=args.substrips)
     torch.cuda.synchronize()
 
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -118,7 +126,7 @@ def run_single(args):
     t0 = time.perf_counter()
     for e0, e1 in evs:
         e0.record(stream)
-        ctx.fill(s1, s2, tab, scheme, waves=args.waves, sync=False)
+        ctx.fill(s1, s2, tab, scheme, waves=args.waves, sync=False, substrips=args.substrips)
         e1.record(stream)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0

@@ -181,14 +181,19 @@ void nw_ctx_destroy(nw_ctx *c) {
     delete c;
 }
 
-int nw_fill_device_async(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *d_s2,
-                         int64_t n2, const nw_params *p, int32_t *d_t, int64_t pitch,
-                         void *stream) {
+static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *d_s2, int64_t n2,
+                       const nw_params *p, const nw_band *band, int32_t *d_t, int64_t pitch,
+                       void *stream) {
     if (!c || !d_t || n1 < 0 || n2 < 0 || n1 >= INT32_MAX || n2 >= INT32_MAX) return NW_ERR_ARG;
     if ((n1 > 0 && !d_s1) || (n2 > 0 && !d_s2)) return NW_ERR_ARG;
     if (!valid_params(p)) return NW_ERR_ARG;
     if (pitch < nw_table_pitch(n1) || pitch % nw::kWave != 0) return NW_ERR_ARG;
     if (((uintptr_t)d_t & 255u) != 0) return NW_ERR_ARG;
+    if (band) {
+        if (band->tag == 0 || (((uintptr_t)band->halo_in | (uintptr_t)band->halo_out) & 7u) != 0)
+            return NW_ERR_ARG;
+        if (band->halo_out && (p->flags & 1)) return NW_ERR_ARG;  // needs the real last row
+    }
     NW_HIP_TRY(hipSetDevice(c->device));
     const Shape s = make_shape(n1, n2, p->waves, p->substrips, c->cus);
     if (s.nstrips > INT32_MAX / 2 || s.nblocks > INT32_MAX / 2) return NW_ERR_ARG;
@@ -232,7 +237,9 @@ int nw_fill_device_async(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t
     a.M = (int32_t)s.M;
     a.tagbase = c->tagbase;
     a.ctrl = c->ctrl;
-    a.top = nullptr;
+    a.halo_in = band ? band->halo_in : nullptr;
+    a.halo_out = band ? band->halo_out : nullptr;
+    a.halo_tag = band ? band->tag : 0u;
     a.scratch = c->scratch;
     a.trace = c->trace;
     a.match = p->match;
@@ -244,6 +251,79 @@ int nw_fill_device_async(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t
     c->last_waves = (int)s.waves;
     c->last_strips = (int)s.nstrips;
     c->last_sub = s.K;
+    return NW_OK;
+}
+
+int nw_fill_device_async(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *d_s2,
+                         int64_t n2, const nw_params *p, int32_t *d_t, int64_t pitch,
+                         void *stream) {
+    return launch_fill(c, d_s1, n1, d_s2, n2, p, nullptr, d_t, pitch, stream);
+}
+
+int nw_fill_band_async(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *d_s2_band,
+                       int64_t n2_band, const nw_params *p, const nw_band *band, int32_t *d_t,
+                       int64_t pitch, void *stream) {
+    if (!band) return NW_ERR_ARG;
+    return launch_fill(c, d_s1, n1, d_s2_band, n2_band, p, band, d_t, pitch, stream);
+}
+
+void nw_band_layout(int64_t n2, int32_t nbands, int32_t r, int64_t *n_rows, int64_t *start) {
+    // mpi-horz-driver.cpp:31-32 / mpi-horz.cpp:16: base = (n2+1)/P rows per band; bands
+    // after the first carry one extra (halo) row; the last band takes the remainder.
+    int64_t rows = 0, st = 0;
+    if (nbands > 0 && r >= 0 && r < nbands) {
+        const int64_t total = n2 + 1, base = total / nbands;
+        rows = base + (r > 0 ? 1 : 0) + (r == nbands - 1 ? total % nbands : 0);
+        st = base * r - (r > 0 ? 1 : 0);
+    }
+    if (n_rows) *n_rows = rows;
+    if (start) *start = st;
+}
+
+int64_t nw_halo_bytes(int64_t n1) { return n1 < 0 ? 0 : (n1 + 1) * (int64_t)sizeof(uint64_t); }
+
+int nw_halo_alloc(int device, int64_t n1, uint64_t **d_halo) {
+    if (!d_halo || n1 < 0) return NW_ERR_ARG;
+    *d_halo = nullptr;
+    if (device >= 0) NW_HIP_TRY(hipSetDevice(device));
+    void *p = nullptr;
+    const size_t bytes = (size_t)nw_halo_bytes(n1);
+    hipError_t e = hipMalloc(&p, bytes);  // its own allocation: exportable by IPC as is
+    if (e != hipSuccess) return e == hipErrorOutOfMemory ? NW_ERR_OOM : NW_ERR_HIP;
+    if (hipMemset(p, 0, bytes) != hipSuccess) {
+        (void)hipFree(p);
+        return NW_ERR_HIP;
+    }
+    *d_halo = (uint64_t *)p;
+    return NW_OK;
+}
+
+int nw_halo_free(uint64_t *d_halo) {
+    if (!d_halo) return NW_ERR_ARG;
+    NW_HIP_TRY(hipFree(d_halo));
+    return NW_OK;
+}
+
+int nw_ipc_get_handle(const void *d_ptr, void *handle) {
+    if (!d_ptr || !handle) return NW_ERR_ARG;
+    hipIpcMemHandle_t h;
+    NW_HIP_TRY(hipIpcGetMemHandle(&h, const_cast<void *>(d_ptr)));
+    std::memcpy(handle, &h, sizeof h < NW_IPC_HANDLE_BYTES ? sizeof h : NW_IPC_HANDLE_BYTES);
+    return NW_OK;
+}
+
+int nw_ipc_open_handle(const void *handle, void **d_ptr) {
+    if (!handle || !d_ptr) return NW_ERR_ARG;
+    hipIpcMemHandle_t h;
+    std::memset(&h, 0, sizeof h);
+    std::memcpy(&h, handle, sizeof h < NW_IPC_HANDLE_BYTES ? sizeof h : NW_IPC_HANDLE_BYTES);
+    NW_HIP_TRY(hipIpcOpenMemHandle(d_ptr, h, hipIpcMemLazyEnablePeerAccess));
+    return NW_OK;
+}
+
+int nw_ipc_close_handle(void *d_ptr) {
+    if (!d_ptr) return NW_ERR_ARG;
+    NW_HIP_TRY(hipIpcCloseMemHandle(d_ptr));
     return NW_OK;
 }
 
@@ -335,7 +415,7 @@ int nw_fill(const int8_t *s1, int64_t n1, const int8_t *s2, int64_t n2, const nw
 }
 
 // Debug hook (not part of the public ABI): per-strip trace buffer, device memory
-// of nstrips * 4 uint64 {start, end, slow waits, wait ticks (100 MHz)}; NULL = off.
+// of nstrips * 8 uint64 (see nwhip.Context.set_trace); NULL = off.
 int nw_debug_set_trace(nw_ctx *c, void *d_trace) {
     if (!c) return NW_ERR_ARG;
     c->trace = (uint64_t *)d_trace;

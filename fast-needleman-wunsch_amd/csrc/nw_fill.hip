@@ -47,6 +47,16 @@ constexpr uint64_t kTimeoutTicks = 100000000ull * 20ull;
 constexpr int kRingWords = kRing * kWave;  // int32 words of one sub-strip's staging ring
 constexpr int kRingBytes = kRingWords * 4;
 
+// Optional cap on this wave's outstanding VMEM operations (stores, mostly),
+// enforced after every flush group: a poll of the left neighbour's granules
+// waits (vmcnt is in-order) for every older store of the wave, so the depth of
+// the store queue is hand-off latency.  0 = no cap (hipcc's own waits only).
+#ifndef NW_VMCAP
+#define NW_VMCAP 0
+#endif
+// s_waitcnt immediate (gfx9): vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[5:4]<<14
+constexpr int vmcnt_imm(int n) { return (n & 15) | (7 << 4) | (15 << 8) | ((n >> 4) << 14); }
+
 __device__ __forceinline__ uint64_t gran_load(const uint64_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -151,13 +161,20 @@ template <int K, bool UNIT, int MODES>
 __device__ __forceinline__ void run_iter(int32_t *__restrict__ lds, int it,
                                          const uint32_t (&pk)[K][16], int32_t msp, int32_t mmp,
                                          int32_t gap, Lanes<K> &S, uint32_t laddr,
-                                         int32_t *const (&fdst)[K], const int64_t (&fpitch)[K],
+                                         char *const (&fdst)[K], const int64_t (&fstep)[K],
+                                         const uint32_t (&foff)[K],
                                          int lane) {
     // Interleaved flush: the ring half this iteration overwrites holds the block
     // that completed in the previous iteration.  Before the 4 steps of group g
     // overwrite its rows 4g..4g+3, those rows are read (ds_read_b128, 4 rows x
     // 64 columns) and stored (global_store_dwordx4, 4 x 256 B row segments), so
     // the 16 stores of a block trickle out one per 4 steps instead of in a burst.
+    //   Addressing: fdst[k] is the block's uniform base (SGPRs; column c0+64k of
+    //   the block's first row), foff[k] this lane's 32-bit byte offset (row rsub,
+    //   column csub), fstep[k] the uniform byte stride of a 4-row group, so each
+    //   store is global_store_dwordx4 voff, data, s[base] with no VALU address
+    //   math.  The LDS read of group g+1 is issued during group g (in-order LDS
+    //   returns), so the store never waits on a just-issued ds_read.
     const int rsub = lane >> 4, csub = (lane & 15) * 4;
     const int fbase = (((it & 1) << 6) + rsub) * 64 + csub;
     // feed of sub-strip 0 (left super-strip's t[i][c0-1] + GAP for the 64 rows
@@ -167,15 +184,20 @@ __device__ __forceinline__ void run_iter(int32_t *__restrict__ lds, int it,
     // keep the 64 per-step ring offsets in-loop (2 VALU/step shared by all K
     // sub-strips) instead of letting hipcc hoist 64 address VGPRs
     asm volatile("" : "+v"(laddr));
+    int4 fv[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) fv[k] = *(const int4 *)(lds + k * kRingWords + fbase);
     static_for<0, 16>([&](auto gc) {
         constexpr int g = decltype(gc)::value;
         const int4 fcur = fq;
         if constexpr (g + 1 < 16) fq = feed4[g + 1];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            const int4 v = *(const int4 *)(lds + k * kRingWords + fbase + g * 256);
-            *(int4 *)(fdst[k] + (int64_t)(4 * g + rsub) * fpitch[k] + csub) = v;
+            const int4 v = fv[k];
+            if constexpr (g + 1 < 16) fv[k] = *(const int4 *)(lds + k * kRingWords + fbase + (g + 1) * 256);
+            *(int4 *)(fdst[k] + g * fstep[k] + foff[k]) = v;
         }
+        if constexpr (NW_VMCAP > 0) __builtin_amdgcn_s_waitcnt(vmcnt_imm(NW_VMCAP));
         static_for<0, 4>([&](auto qc) {
             constexpr int q = decltype(qc)::value;
             constexpr int u = 4 * g + q;
@@ -234,14 +256,41 @@ __device__ void process_strip(const FillArgs &A, int32_t *__restrict__ lds, int 
     const int32_t gap = A.gap;
     const int32_t msp = A.match - gap, mmp = A.mismatch - gap;
     const int64_t c0 = (int64_t)p * (64 * K);
+    bool dead = false;
+    // Row 0: the boundary t[0][c] = c*GAP (serial.cpp:16), or -- for a row band
+    // (mpi-horz.cpp:16-40) -- the previous band's last row, taken from its halo
+    // granules once they carry this launch's tag (bounded wait).
+    int32_t top[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) top[k] = (int32_t)((c0 + 64 * k + lane) * (int64_t)gap);
+    if (A.halo_in != nullptr) {
+        const uint64_t h0 = __builtin_amdgcn_s_memrealtime();
+        for (;;) {
+            bool ok = true;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int64_t c = min(c0 + 64 * k + lane, A.n1);
+                const uint64_t g = __hip_atomic_load(A.halo_in + c, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_SYSTEM);
+                top[k] = (int32_t)(uint32_t)g;
+                ok &= (uint32_t)(g >> 32) == A.halo_tag;
+            }
+            if (__all(ok)) break;
+            if (ctrl_load(A.ctrl + 1) != 0u) { dead = true; break; }
+            if (__builtin_amdgcn_s_memrealtime() - h0 > kTimeoutTicks) {
+                if (lane == 0) atomicCAS(A.ctrl + 1, 0u, 2u);
+                dead = true;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(4);
+        }
+    }
     Lanes<K> S;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const int64_t c = c0 + 64 * k + lane;
         S.a[k] = (c >= 1 && c <= A.n1) ? (uint32_t)A.s1[c - 1] : 0u;
-        int32_t top = (int32_t)(c * (int64_t)gap);
-        if (A.top != nullptr && c <= A.n1) top = A.top[c];
-        S.tg[k] = top + gap;  // t[0][c] + GAP
+        S.tg[k] = top[k] + gap;  // t[0][c] + GAP
         S.tl[k] = 0;
         S.rr[k] = -lane - 1;
     }
@@ -285,10 +334,11 @@ __device__ void process_strip(const FillArgs &A, int32_t *__restrict__ lds, int 
         load_packs(A.rowpack, 1 - k, lane, pkb[2][k]);
     }
 
-    bool dead = false;
     uint32_t nslow = 0;
     uint64_t wticks = 0;
     const uint64_t tstart = __builtin_amdgcn_s_memrealtime();
+    const uint64_t cstart = __builtin_amdgcn_s_memtime();
+    uint64_t tq1 = 0, tmid = 0;  // trace: times iterations nblocks/4 and nblocks/2 started
 
     // One iteration: feed for block it, prefetch for it+2, flush (interleaved
     // with the steps), 64 steps.  A watchdog trip only marks the strip dead; the
@@ -299,6 +349,10 @@ __device__ void process_strip(const FillArgs &A, int32_t *__restrict__ lds, int 
         constexpr int CONS = decltype(cons_c)::value;  // (it + 1) % 3
         constexpr int ISS = decltype(iss_c)::value;    // it % 3
         constexpr int MODES = decltype(modes)::value;
+        if (A.trace != nullptr) {
+            if (it == A.nblocks / 4) tq1 = __builtin_amdgcn_s_memrealtime();
+            if (it == A.nblocks / 2) tmid = __builtin_amdgcn_s_memrealtime();
+        }
         if (it < A.nblocks) {
             int32_t fvv = kNeg;
             if (has_left) {
@@ -324,14 +378,17 @@ __device__ void process_strip(const FillArgs &A, int32_t *__restrict__ lds, int 
         // table (not yet started / past the end / columns past the pitch) go to
         // this workgroup's scratch tile, so every iteration issues the same
         // K*16 + 1 stores.
-        int32_t *fdst[K];
-        int64_t fpitch[K];
+        char *fdst[K];
+        int64_t fstep[K];
+        uint32_t foff[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const int b = it - 2 - k;
             const bool ok = valid[k] && b >= 0 && b < A.nblocks && !(A.flags & 1);
-            fdst[k] = ok ? A.table + (int64_t)b * 64 * A.pitch + c0 + 64 * k : scr;
-            fpitch[k] = ok ? A.pitch : (int64_t)kWave;
+            fdst[k] = (char *)(ok ? A.table + (int64_t)b * 64 * A.pitch + c0 + 64 * k : scr);
+            const int64_t fp = ok ? A.pitch : (int64_t)kWave;
+            fstep[k] = 16 * fp;  // bytes of 4 rows
+            foff[k] = (uint32_t)(((lane >> 4) * fp + (lane & 15) * 4) * 4);
         }
         {
             // right column of the super-strip (sub-strip K-1, lane 63) for block b,
@@ -345,7 +402,7 @@ __device__ void process_strip(const FillArgs &A, int32_t *__restrict__ lds, int 
             gran_store(gp, ((uint64_t)tag_out << 32) | (uint32_t)v);
         }
         run_iter<K, UNIT, MODES>(lds, it, pkb[CONS], msp, mmp, gap, S,
-                                 lbase + (uint32_t)(it & 1) * (64u * 256u), fdst, fpitch, lane);
+                                 lbase + (uint32_t)(it & 1) * (64u * 256u), fdst, fstep, foff, lane);
     };
 
     // sub-strip K-1 completes the last block in iteration nblocks-1+K; it is
@@ -372,12 +429,36 @@ __device__ void process_strip(const FillArgs &A, int32_t *__restrict__ lds, int 
         iter(it + 2, std::integral_constant<int, (P0 + 3) % 3>{},
              std::integral_constant<int, (P0 + 2) % 3>{}, std::integral_constant<int, RUNALL>{});
     }
+    // Row band: hand this strip's columns of the last row (n2) to the next band.
+    // The table stores are plain (write-back L2), so: drain them, write the XCD's
+    // L2 back (agent release), re-read the row with sc1 loads, publish
+    // system-scope granules (write-through; peer HBM over xGMI when the next
+    // band lives on another GPU).
+    if (A.halo_out != nullptr && !dead) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const int32_t *last = A.table + A.n2 * A.pitch;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int64_t c = c0 + 64 * k + lane;
+            if (c <= A.n1) {
+                const uint32_t v = (uint32_t)__hip_atomic_load(last + c, __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(A.halo_out + c, ((uint64_t)A.halo_tag << 32) | v,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+    }
     if (A.trace != nullptr && lane == 0) {
-        uint64_t *tr = A.trace + (int64_t)p * 4;
+        uint64_t *tr = A.trace + (int64_t)p * kTraceWords;
         tr[0] = tstart;
         tr[1] = __builtin_amdgcn_s_memrealtime();
         tr[2] = nslow;
         tr[3] = wticks;
+        tr[4] = tq1;
+        tr[5] = tmid;
+        tr[6] = cstart;                          // shader clock (s_memtime)
+        tr[7] = __builtin_amdgcn_s_memtime();
     }
 }
 

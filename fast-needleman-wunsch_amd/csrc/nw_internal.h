@@ -11,6 +11,7 @@ constexpr int kQOff = 64;          // rowpack index offset (lane l reads index 4
 constexpr int32_t kNeg = -(1 << 29);  // "minus infinity" fed left of column 0
 constexpr int kScratchWords = kWave * kWave + 2 * kWave;  // per workgroup (16.5 KB)
 constexpr int kMaxSub = 4;        // max 64-column sub-strips per wave (LDS: 32 KB each)
+constexpr int kTraceWords = 8;     // debug trace words per strip
 
 // Everything one launch of the strip-sweep kernel needs.  Plain POD, passed by
 // value as the kernel argument.
@@ -29,9 +30,13 @@ struct FillArgs {
     int32_t M;                 // number of slots (>= waves + 1, or nstrips)
     uint32_t tagbase;          // strip p publishes tag tagbase + p + 1
     uint32_t *ctrl;            // [0] strip ticket, [1] error word, [2..3] spare
-    const int32_t *top;        // optional device row 0 (nCols values) for row bands; NULL = j*gap
+    // Row bands (mpi-horz contract): row 0 of this launch is the previous band's
+    // last row, delivered as granules {tag:32 | value:32}, one per column 0..n1.
+    const uint64_t *halo_in;   // NULL = row 0 is the boundary j*gap (first band / whole table)
+    uint64_t *halo_out;        // NULL, or the next band's halo_in (peer memory): row n2 goes here
+    uint32_t halo_tag;         // launch tag shared with the neighbouring bands (> 0)
     int32_t *scratch;          // per-workgroup dummy flush target: grid * kScratchWords int32
-    uint64_t *trace;           // optional per-strip trace [nstrips][4]: start, end, slow waits, wait ticks
+    uint64_t *trace;           // optional per-strip debug trace [nstrips][kTraceWords]
     int32_t match, mismatch, gap;
     int32_t flags;             // debug: bit0 = send table stores to the scratch tile (timing only)
 };

@@ -18,7 +18,8 @@ from dataclasses import dataclass
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "build", "libnwhip.so")
+# NWHIP_LIB selects an alternative in-tree build (tuning variants from `make variant`)
+LIB_PATH = os.environ.get("NWHIP_LIB") or os.path.join(HERE, "build", "libnwhip.so")
 
 NW_OK, NW_ERR_ARG, NW_ERR_HIP, NW_ERR_OOM, NW_ERR_TIMEOUT, NW_ERR_NODEVICE, NW_ERR_UNSUPPORTED = range(7)
 
@@ -26,7 +27,10 @@ NW_OK, NW_ERR_ARG, NW_ERR_HIP, NW_ERR_OOM, NW_ERR_TIMEOUT, NW_ERR_NODEVICE, NW_E
 EXPORTS = ["nw_params_default", "nw_strerror", "nw_version", "nw_fill", "nw_table_pitch",
            "nw_table_bytes", "nw_ctx_create", "nw_ctx_destroy", "nw_ctx_workspace_bytes",
            "nw_fill_device", "nw_fill_device_async", "nw_ctx_status", "nw_read_bdna", "nw_free",
-           "nw_synth_bdna"]
+           "nw_synth_bdna", "nw_band_layout", "nw_halo_bytes", "nw_fill_band_async",
+           "nw_ipc_get_handle", "nw_ipc_open_handle", "nw_ipc_close_handle", "nw_halo_alloc",
+           "nw_halo_free"]
+IPC_HANDLE_BYTES = 64
 
 
 class NwParams(ctypes.Structure):
@@ -40,6 +44,12 @@ class NwResult(ctypes.Structure):
                 ("kernel_ms", ctypes.c_double), ("table_bytes", ctypes.c_double),
                 ("strips", ctypes.c_int32), ("waves", ctypes.c_int32),
                 ("substrips", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class NwBand(ctypes.Structure):
+    """nw_band (include/nw_hip.h): halo granule buffers of one row band."""
+    _fields_ = [("halo_in", ctypes.c_void_p), ("halo_out", ctypes.c_void_p),
+                ("tag", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
 
 
 class NwError(RuntimeError):
@@ -96,6 +106,20 @@ def lib() -> ctypes.CDLL:
     L.nw_free.restype = None
     L.nw_synth_bdna.argtypes = [ctypes.c_uint64, ctypes.c_int64, _i8p]
     L.nw_synth_bdna.restype = None
+    L.nw_band_layout.argtypes = [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                 ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
+    L.nw_band_layout.restype = None
+    L.nw_halo_bytes.argtypes = [ctypes.c_int64]
+    L.nw_halo_bytes.restype = ctypes.c_int64
+    L.nw_fill_band_async.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                     ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(NwParams),
+                                     ctypes.POINTER(NwBand), ctypes.c_void_p, ctypes.c_int64,
+                                     ctypes.c_void_p]
+    L.nw_ipc_get_handle.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+    L.nw_ipc_open_handle.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]
+    L.nw_ipc_close_handle.argtypes = [ctypes.c_void_p]
+    L.nw_halo_alloc.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p)]
+    L.nw_halo_free.argtypes = [ctypes.c_void_p]
     _lib = L
     return L
 
@@ -183,6 +207,64 @@ def read_bdna(path: str) -> np.ndarray:
     return out
 
 
+def band_layout(n2: int, nbands: int, r: int):
+    """(rows incl. the halo row, global index of row 0) of band r -- the row
+    partition of src/mpi/mpi-horz-driver.cpp:31-32 / mpi-horz.cpp:16."""
+    rows, start = ctypes.c_int64(), ctypes.c_int64()
+    lib().nw_band_layout(n2, nbands, r, ctypes.byref(rows), ctypes.byref(start))
+    return int(rows.value), int(start.value)
+
+
+def halo_bytes(n1: int) -> int:
+    return int(lib().nw_halo_bytes(n1))
+
+
+class Halo:
+    """A zeroed halo granule buffer (n1+1 x {tag, value}) in its own allocation."""
+
+    def __init__(self, n1: int, device: int = -1):
+        ptr = ctypes.c_void_p()
+        st = lib().nw_halo_alloc(device, n1, ctypes.byref(ptr))
+        if st != NW_OK:
+            raise NwError(st, "nw_halo_alloc")
+        self.ptr, self.n1 = int(ptr.value), n1
+
+    def free(self):
+        if self.ptr:
+            lib().nw_halo_free(ctypes.c_void_p(self.ptr))
+            self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def ipc_get_handle(ptr: int) -> bytes:
+    """Export a device allocation (e.g. a halo buffer) to another process."""
+    buf = ctypes.create_string_buffer(IPC_HANDLE_BYTES)
+    st = lib().nw_ipc_get_handle(ctypes.c_void_p(ptr), buf)
+    if st != NW_OK:
+        raise NwError(st, "nw_ipc_get_handle")
+    return buf.raw
+
+
+def ipc_open_handle(handle: bytes) -> int:
+    """Map a peer process's exported allocation into this device's address space."""
+    ptr = ctypes.c_void_p()
+    st = lib().nw_ipc_open_handle(handle, ctypes.byref(ptr))
+    if st != NW_OK:
+        raise NwError(st, "nw_ipc_open_handle")
+    return int(ptr.value)
+
+
+def ipc_close_handle(ptr: int) -> None:
+    st = lib().nw_ipc_close_handle(ctypes.c_void_p(ptr))
+    if st != NW_OK:
+        raise NwError(st, "nw_ipc_close_handle")
+
+
 def synth(seed: int, n: int) -> np.ndarray:
     out = np.empty(n, dtype=np.int8)
     lib().nw_synth_bdna(seed, n, out.ctypes.data_as(_i8p))
@@ -241,9 +323,40 @@ class Context:
             raise NwError(st, "nw_fill_device_async")
         return None
 
+    def fill_band(self, d_s1, d_s2_band, table, halo_in=None, halo_out=None, tag: int = 1,
+                  scheme=(1, 0, -1), waves: int = 0, stream=None, flags: int = 0,
+                  substrips: int = 0) -> None:
+        """Launch one row band (asynchronous).  d_s2_band: the band's side
+        characters (len = band rows - 1); table: alloc_table(n1, len(d_s2_band)),
+        row 0 = the halo row.  halo_in / halo_out: int64 CUDA tensors of
+        n1+1 granules or raw device addresses (peer memory from ipc_open_handle)."""
+        import torch
+        n1, n2 = int(d_s1.numel()), int(d_s2_band.numel())
+        assert table.dtype == torch.int32 and table.is_contiguous()
+        assert table.shape[0] >= table_rows(n2) and table.shape[1] == table_pitch(n1)
+
+        def addr(x):
+            if x is None:
+                return None
+            if isinstance(x, int):
+                return x
+            assert x.dtype == torch.int64 and x.numel() >= n1 + 1
+            return x.data_ptr()
+        if stream is None:
+            stream = torch.cuda.current_stream(table.device)
+        b = NwBand(addr(halo_in), addr(halo_out), int(tag), 0)
+        p = params(scheme, waves, self.device, flags, substrips)
+        st = lib().nw_fill_band_async(self._h, ctypes.c_void_p(d_s1.data_ptr() if n1 else 0), n1,
+                                      ctypes.c_void_p(d_s2_band.data_ptr() if n2 else 0), n2,
+                                      ctypes.byref(p), ctypes.byref(b),
+                                      ctypes.c_void_p(table.data_ptr()), table.shape[1],
+                                      ctypes.c_void_p(stream.cuda_stream))
+        if st != NW_OK:
+            raise NwError(st, "nw_fill_band_async")
+
     def set_trace(self, trace_tensor) -> None:
-        """Debug: record {start, end, slow waits, wait ticks} per strip into a
-        uint64/int64 CUDA tensor of nstrips*4 elements (None = off)."""
+        """Debug: record {start, end, slow waits, wait ticks, t(quarter), t(mid)}
+        per strip into a uint64/int64 CUDA tensor of nstrips*8 elements (None = off)."""
         L = lib()
         L.nw_debug_set_trace.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         L.nw_debug_set_trace(self._h, ctypes.c_void_p(trace_tensor.data_ptr() if trace_tensor is not None else 0))

@@ -122,6 +122,49 @@ int nw_fill_device_async(nw_ctx *ctx, const int8_t *d_s1, int64_t n1,
                          const int8_t *d_s2, int64_t n2, const nw_params *p,
                          int32_t *d_t, int64_t pitch, void *stream);
 
+/* Row bands (multi-GPU) ---------------------------------------------------
+ * The reference's 8-GPU twin is src/mpi/mpi-horz.cpp:4-99 (+ mpi-horz-driver.cpp):
+ * rank r fills a contiguous band of rows whose row 0 is rank r-1's last row (the
+ * halo), received in chunks while r-1 is still filling.  Here band r's kernel
+ * takes that row from `halo_in` -- granules {tag:32 | value:32}, one per column
+ * 0..n1 -- as each 64-column strip starts, and publishes its own last row into
+ * `halo_out` (the next band's halo_in, usually peer memory on the next GPU
+ * mapped with nw_ipc_open_handle) as each strip finishes: a pipelined halo with
+ * no host round trip.  `tag` identifies the launch (> 0, the same value on both
+ * sides of a halo, new for every launch); halo buffers must start zeroed. */
+typedef struct nw_band {
+    const uint64_t *halo_in;  /* NULL: row 0 is the boundary j*gap (first band)  */
+    uint64_t *halo_out;       /* NULL: last band                                  */
+    uint32_t tag;
+    uint32_t reserved;
+} nw_band;
+
+/* Band layout of mpi-horz-driver.cpp:31-32: rows of band r (including its halo
+ * row) and the global index of its row 0, for a table of n2+1 rows in nbands. */
+void nw_band_layout(int64_t n2, int32_t nbands, int32_t r, int64_t *n_rows, int64_t *start);
+
+/* Bytes of one halo granule buffer for n1 (+1) columns. */
+int64_t nw_halo_bytes(int64_t n1);
+
+/* A zeroed halo granule buffer of its own hipMalloc (so that nw_ipc_get_handle
+ * exports exactly it); device -1 = current. */
+int nw_halo_alloc(int device, int64_t n1, uint64_t **d_halo);
+int nw_halo_free(uint64_t *d_halo);
+
+/* Fill one band: d_t holds n2_band+1 rows (row 0 = the halo row, written by
+ * the kernel from halo_in), d_s2_band = the band's side characters
+ * (s2 + start of the band: local row i >= 1 uses d_s2_band[i-1]).  Async. */
+int nw_fill_band_async(nw_ctx *ctx, const int8_t *d_s1, int64_t n1, const int8_t *d_s2_band,
+                       int64_t n2_band, const nw_params *p, const nw_band *band, int32_t *d_t,
+                       int64_t pitch, void *stream);
+
+/* Cross-process device pointers (one process per GPU): export a device
+ * allocation, open a peer's export.  Handles are NW_IPC_HANDLE_BYTES bytes. */
+#define NW_IPC_HANDLE_BYTES 64
+int nw_ipc_get_handle(const void *d_ptr, void *handle);
+int nw_ipc_open_handle(const void *handle, void **d_ptr);
+int nw_ipc_close_handle(void *d_ptr);
+
 /* Check the in-kernel watchdog word of the last launch (syncs the stream). */
 int nw_ctx_status(nw_ctx *ctx, void *stream);
 

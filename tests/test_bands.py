@@ -1,0 +1,177 @@
+"""Row bands (multi-GPU path, mpi-horz contract: src/mpi/mpi-horz.cpp:4-99,
+mpi-horz-driver.cpp:31-32,88-90).
+
+CPU (-m "not gpu"): the band layout of the C ABI against the oracle; the band /
+halo contract over a real world_size-2 and -3 gloo process group (each rank fills
+its band with the oracle, the halo row travels rank to rank as the GPU path's
+halo granules do), checked against the whole-table oracle.
+GPU (-m gpu): LocalBands -- several bands concurrently on one device through the
+in-kernel halo hand-off -- bit-exact against the oracle's bands; and the
+multi-process bench path (2 ranks sharing the one GPU: IPC halo buffers, gloo
+control plane) checked against the oracle's score.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import nwhip
+import oracle
+from conftest import PKG, ROOT
+
+sys.path.insert(0, PKG)
+import nw_bands  # noqa: E402
+
+
+# ------------------------------------------------------------------ layout (CPU)
+@pytest.mark.parametrize("n2,P", [(0, 1), (7, 8), (10, 2), (63, 4), (100, 3), (1000, 7),
+                                  (524288, 8), (262144, 4), (131072, 2), (65535, 8)])
+def test_band_layout_matches_oracle(n2, P):
+    for r in range(P):
+        assert nwhip.band_layout(n2, P, r) == oracle.band_layout(n2, P, r)
+
+
+@pytest.mark.parametrize("n2,P", [(10, 2), (100, 3), (1000, 7), (524288, 8), (17, 8)])
+def test_bands_tile_the_rows(n2, P):
+    """Band r>0 starts on band r-1's last row (the halo); the last band ends on row n2."""
+    lay = nw_bands.plan(n2, P)
+    assert lay[0][1] == 0
+    for (rows_a, st_a), (rows_b, st_b) in zip(lay, lay[1:]):
+        assert st_b == st_a + rows_a - 1
+    rows, st = lay[-1]
+    assert st + rows - 1 == n2
+
+
+# ------------------------------------------------------------------ gloo ranks (CPU)
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank_main(rank, world, port, n1, n2, scheme, outdir):
+    import torch.distributed as dist
+    import torch
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    s1, s2 = oracle.synth(11, n1), oracle.synth(12, n2)
+    rows, start = nwhip.band_layout(n2, world, rank)
+    halo = None
+    if rank > 0:  # halo row = rank-1's last row (mpi-horz.cpp:28-40)
+        h = torch.empty(n1 + 1, dtype=torch.int32)
+        dist.recv(h, src=rank - 1)
+        halo = h.numpy()
+    band = oracle.fill_band(s1, s2, world, rank, halo, scheme)
+    assert band.shape == (rows, n1 + 1)
+    if rank + 1 < world:
+        dist.send(torch.from_numpy(band[-1].copy()), dst=rank + 1)
+    np.save(os.path.join(outdir, f"band{rank}.npy"), band)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_bands_reassemble_the_table(tmp_path, world):
+    import torch.multiprocessing as mp
+    n1, n2, scheme = 301, 257, (1, -1, -1)
+    mp.spawn(_rank_main, args=(world, _free_port(), n1, n2, scheme, str(tmp_path)),
+             nprocs=world, join=True)
+    full = oracle.fill(oracle.synth(11, n1), oracle.synth(12, n2), scheme)
+    for r in range(world):
+        rows, start = nwhip.band_layout(n2, world, r)
+        band = np.load(tmp_path / f"band{r}.npy")
+        np.testing.assert_array_equal(band, full[start:start + rows])
+    # final score on the last rank's last cell (mpi-horz-driver.cpp:88-90)
+    assert np.load(tmp_path / f"band{world - 1}.npy")[-1, -1] == full[-1, -1]
+
+
+# ------------------------------------------------------------------ GPU
+@pytest.fixture(scope="module")
+def torch_gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n1,n2,P", [(300, 200, 2), (1000, 777, 3), (640, 130, 4), (129, 7, 8),
+                                     (64 * 37 + 5, 999, 5)])
+@pytest.mark.parametrize("scheme", [(1, 0, -1), (1, -1, -1), (2, -1, -2)])
+def test_local_bands_vs_oracle(torch_gpu, n1, n2, P, scheme):
+    torch = torch_gpu
+    rng = np.random.default_rng(n1 * 31 + n2 + P)
+    s1 = rng.integers(1, 5, n1).astype(np.int8)
+    s2 = rng.integers(1, 5, n2).astype(np.int8)
+    lb = nw_bands.LocalBands(n1, n2, P)
+    try:
+        score = lb.fill(torch.from_numpy(s1).cuda(), torch.from_numpy(s2).cuda(), scheme)
+        full = oracle.fill(s1, s2, scheme)
+        assert score == full[-1, -1]
+        for r, (rows, start) in enumerate(lb.layout):
+            got = lb.tables[r][:rows, :n1 + 1].cpu().numpy()
+            np.testing.assert_array_equal(got, full[start:start + rows], err_msg=f"band {r}")
+    finally:
+        lb.close()
+
+
+@pytest.mark.gpu
+def test_local_bands_repeated_launches(torch_gpu):
+    """Tags advance per launch; stale halo granules of earlier launches are never taken."""
+    torch = torch_gpu
+    n1, n2, P = 2000, 1500, 3
+    lb = nw_bands.LocalBands(n1, n2, P)
+    try:
+        for seed in range(4):
+            rng = np.random.default_rng(seed)
+            s1 = rng.integers(1, 5, n1).astype(np.int8)
+            s2 = rng.integers(1, 5, n2).astype(np.int8)
+            score = lb.fill(torch.from_numpy(s1).cuda(), torch.from_numpy(s2).cuda())
+            full = oracle.fill(s1, s2)
+            assert score == full[-1, -1]
+            for r, (rows, start) in enumerate(lb.layout):
+                np.testing.assert_array_equal(lb.tables[r][:rows, :n1 + 1].cpu().numpy(),
+                                              full[start:start + rows])
+    finally:
+        lb.close()
+
+
+@pytest.mark.gpu
+def test_local_bands_32k_score(torch_gpu):
+    """BASELINE config-2 inputs split into 4 concurrent bands on one GPU."""
+    torch = torch_gpu
+    n = 32768
+    s1, s2 = nwhip.synth(1, n), nwhip.synth(2, n)
+    lb = nw_bands.LocalBands(n, n, 4)
+    try:
+        score = lb.fill(torch.from_numpy(s1).cuda(), torch.from_numpy(s2).cuda())
+        assert score == 13394  # reference serial.cpp on the same inputs (synth_scores.json)
+        sc, lr, lc, rs, rw = oracle.score(s1, s2, want_rows=True)
+        rows, start = lb.layout[-1]
+        np.testing.assert_array_equal(lb.tables[-1][rows - 1, :n + 1].cpu().numpy(), lr)
+    finally:
+        lb.close()
+
+
+@pytest.mark.gpu
+def test_two_process_bands_shared_gpu(torch_gpu):
+    """The bench's multi-process path end to end on one GPU: 2 ranks (torch.distributed.run,
+    gloo control plane), IPC-mapped halo buffer, in-kernel halo stores."""
+    n1, rows = 4096 + 17, 700
+    env = dict(os.environ, PYTHONPATH=PKG)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--share-gpu", "--band-rows", str(rows), "--band-cols", str(n1)]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1]
+    res = json.loads(line)
+    n2 = 2 * rows
+    want = oracle.score(nwhip.synth(1, n1), nwhip.synth(2, n2))
+    assert res["score"] == want and res["n_gpus"] == 2 and res["config"]["n2"] == n2

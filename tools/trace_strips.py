@@ -15,6 +15,7 @@ ap.add_argument("--n", type=int, default=32768)
 ap.add_argument("--waves", default="0")
 ap.add_argument("--flags", type=int, default=0)
 ap.add_argument("--sub", type=int, default=0)
+ap.add_argument("--save", default="")
 args = ap.parse_args()
 ctx = nwhip.Context(0)
 n = args.n
@@ -22,7 +23,7 @@ s1 = torch.from_numpy(nwhip.synth(1, n)).cuda()
 s2 = torch.from_numpy(nwhip.synth(2, n)).cuda()
 tab = nwhip.Context.alloc_table(n, n)
 nstrips = (n + 1 + 63) // 64
-tr = torch.zeros(nstrips * 4, dtype=torch.int64, device="cuda")
+tr = torch.zeros(nstrips * 8, dtype=torch.int64, device="cuda")
 for w in [int(x) for x in args.waves.split(",")]:
     ctx.set_trace(None)
     r0 = ctx.fill(s1, s2, tab, waves=w, flags=args.flags, substrips=args.sub)
@@ -30,17 +31,36 @@ for w in [int(x) for x in args.waves.split(",")]:
     r = ctx.fill(s1, s2, tab, waves=w, flags=args.flags, substrips=args.sub)
     nstrips = r.strips
     ctx.set_trace(None)
-    t = tr[: nstrips * 4].view(nstrips, 4).cpu().numpy().astype(np.float64)
+    t = tr[: nstrips * 8].view(nstrips, 8).cpu().numpy().astype(np.float64)
+    if args.save:
+        np.save(f"{args.save}_w{w}_k{r.substrips}.npy", t)
     t0 = t[:, 0].min()
     st = (t[:, 0] - t0) / 100.0   # us
     en = (t[:, 1] - t0) / 100.0
     dur = en - st
     lag = np.diff(st)
+    # hop lag: time strip p reached the middle (quarter) of the table after strip p-1 did
+    for col, nm in ((5, "mid"), (4, "quarter")):
+        tm = t[:, col]
+        ok = (tm[1:] > 0) & (tm[:-1] > 0)
+        hop = (tm[1:] - tm[:-1])[ok] / 100.0
+        if hop.size:
+            pq = np.percentile(hop, [10, 50, 90])
+            w = r.waves
+            later = hop[w:] if hop.size > w else hop
+            print(f"  hop lag at {nm} (us): mean {hop.mean():.2f} p10 {pq[0]:.2f} med {pq[1]:.2f} p90 {pq[2]:.2f} "
+                  f"p99 {np.percentile(hop, 99):.2f} max {hop.max():.1f}; "
+                  f"first pass med {np.median(hop[:w]):.2f}; later med {np.median(later):.2f}")
     busy = (dur - t[:, 3] / 100.0).sum()
     print(f"  sum(strip time - wait) / (waves * span) = {busy / (r.waves * en.max()):.3f}; "
           f"sum(wait) / (waves*span) = {t[:, 3].sum() / 100.0 / (r.waves * en.max()):.3f}")
     print(f"n={n} K={r.substrips} waves={r.waves} strips={r.strips} kernel_ms={r.kernel_ms:.3f} (untraced {r0.kernel_ms:.3f}) "
           f"span_us={en.max():.0f}")
+    clk = (t[:, 7] - t[:, 6]) / np.maximum(t[:, 1] - t[:, 0], 1) * 100e6 / 1e9
+    print(f"  effective shader clock GHz per strip: strip0 {clk[0]:.3f} p10 {np.percentile(clk, 10):.3f} "
+          f"med {np.median(clk):.3f} p90 {np.percentile(clk, 90):.3f}")
+    busy_row = (dur - t[:, 3] / 100.0) / n * 1000.0
+    print(f"  busy ns/row: strip0 {busy_row[0]:.2f} med {np.median(busy_row):.2f} p90 {np.percentile(busy_row, 90):.2f}")
     print(f"  strip duration us: min {dur.min():.0f} med {np.median(dur):.0f} max {dur.max():.0f}"
           f"  -> per row {np.median(dur)/n*1000:.2f} ns")
     print(f"  start lag us: med {np.median(lag):.2f} p10 {np.percentile(lag,10):.2f} p90 {np.percentile(lag,90):.2f}")
