@@ -22,7 +22,7 @@ struct nw_ctx {
     int cus = 256;
     uint64_t *gran = nullptr;
     size_t gran_cap = 0;  // bytes
-    uint32_t *rowpack = nullptr;
+    void *rowpack = nullptr;
     size_t rowpack_cap = 0;
     int32_t *scratch = nullptr;
     size_t scratch_cap = 0;
@@ -138,7 +138,7 @@ int64_t nw_table_bytes(int64_t n1, int64_t n2) {
 
 int64_t nw_ctx_workspace_bytes(int64_t n1, int64_t n2, int32_t waves) {
     Shape s = make_shape(n1, n2, waves, 0, 256);
-    return s.M * s.gstride * 8 + nw::rowpack_len((int32_t)s.nblocks) * 4 +
+    return s.M * s.gstride * 8 + nw::rowpack_len((int32_t)s.nblocks) * 16 +
            s.waves * nw::kScratchWords * 4 + 16;
 }
 
@@ -211,7 +211,7 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
         c->tagbase = 1;
     }
     const int64_t qlen = nw::rowpack_len((int32_t)s.nblocks);
-    if ((st = grow((void **)&c->rowpack, &c->rowpack_cap, (size_t)qlen * 4, false)) != NW_OK)
+    if ((st = grow((void **)&c->rowpack, &c->rowpack_cap, (size_t)qlen * 16, false)) != NW_OK)
         return st;
     if ((st = grow((void **)&c->scratch, &c->scratch_cap,
                    (size_t)s.waves * nw::kScratchWords * 4, false)) != NW_OK)

@@ -5,12 +5,11 @@
 
 namespace nw {
 
-constexpr int kWave = 64;          // lanes per wavefront = columns per strip
-constexpr int kRing = 128;         // rows held by the LDS staging ring (2 blocks of 64)
+constexpr int kWave = 64;          // lanes per wavefront
 constexpr int kQOff = 64;          // rowpack index offset (lane l reads index 4g - l)
 constexpr int32_t kNeg = -(1 << 29);  // "minus infinity" fed left of column 0
 constexpr int kScratchWords = kWave * kWave + 2 * kWave;  // per workgroup (16.5 KB)
-constexpr int kMaxSub = 4;        // max 64-column sub-strips per wave (LDS: 32 KB each)
+constexpr int kMaxSub = 4;        // max columns per lane (strip = 64 * C columns)
 constexpr int kTraceWords = 8;     // debug trace words per strip
 
 // Everything one launch of the strip-sweep kernel needs.  Plain POD, passed by
@@ -18,7 +17,7 @@ constexpr int kTraceWords = 8;     // debug trace words per strip
 struct FillArgs {
     int32_t *table;            // device table, row-major, row pitch `pitch` (int32 elems)
     int64_t pitch;             // multiple of 64 (256-B aligned rows)
-    const uint32_t *rowpack;   // rowpack[x + kQOff] = B[x] | B[x+1]<<8 | B[x+2]<<16 | B[x+3]<<24,
+    const void *rowpack;       // 16-byte entries: rowpack[x + kQOff] = B[x .. x+15],
                                //   B[x] = s2[x-1] for 1 <= x <= n2, else 0
     const uint8_t *s1;         // n1 column characters
     int64_t n1, n2;            // nCols = n1 + 1, nRows = n2 + 1
@@ -42,11 +41,11 @@ struct FillArgs {
 };
 
 // Launch helpers implemented in nw_fill.hip.  Return hipError_t as int.
-int launch_rowpack(const uint8_t *d_s2, int64_t n2, int64_t row0, uint32_t *d_q, int64_t qlen,
+int launch_rowpack(const uint8_t *d_s2, int64_t n2, int64_t row0, void *d_q, int64_t qlen,
                    void *stream);
 int launch_fill(const FillArgs &a, int substrips, int grid, void *stream);
 int lds_bytes(int substrips);
-int64_t rowpack_len(int32_t nblocks);
+int64_t rowpack_len(int32_t nblocks);  // 16-byte entries
 const char *kernel_variant();
 
 }  // namespace nw

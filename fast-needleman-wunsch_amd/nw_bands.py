@@ -40,11 +40,11 @@ def plan(n2: int, nbands: int):
 
 
 def resident_waves(device: int = 0, substrips: int = 1) -> int:
-    """Persistent workers that fit on the device at once (LDS-bound: one 128-row
-    ring of 64 columns per sub-strip + the feed buffer, as nw::lds_bytes)."""
+    """Persistent workers that fit on the device at once (LDS-bound: a 64-slot
+    anti-diagonal ring of 64*substrips int32 + the feed buffer, as nw::lds_bytes)."""
     import torch
     cus = torch.cuda.get_device_properties(device).multi_processor_count
-    lds = (substrips * 128 * 64 + 128) * 4
+    lds = (substrips * 64 * 64 + 128) * 4
     return cus * (LDS_PER_CU // lds)
 
 
