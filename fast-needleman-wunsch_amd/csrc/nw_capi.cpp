@@ -24,6 +24,9 @@ struct nw_ctx {
     size_t gran_cap = 0;  // bytes
     void *rowpack = nullptr;
     size_t rowpack_cap = 0;
+    void *prof = nullptr;      // query profiles (kMaxProf x rowpack entries)
+    size_t prof_cap = 0;
+    uint8_t *meta = nullptr;   // charmap / chars / nprof (nw::kMetaBytes)
     int32_t *scratch = nullptr;
     size_t scratch_cap = 0;
     uint32_t *ctrl = nullptr;  // 4 words
@@ -86,6 +89,8 @@ Shape make_shape(int64_t n1, int64_t n2, int32_t waves_req, int32_t sub_req, int
     s.gstride = s.nblocks * nw::kWave;
     return s;
 }
+
+bool fits_i8(int32_t x) { return x >= -128 && x <= 127; }
 
 bool valid_params(const nw_params *p) {
     if (!p) return false;
@@ -161,6 +166,7 @@ int nw_ctx_create(int device, nw_ctx **out) {
     c->device = device;
     c->cus = prop.multiProcessorCount;
     if (hipMalloc(&c->ctrl, 16) != hipSuccess || hipMemset(c->ctrl, 0, 16) != hipSuccess ||
+        hipMalloc(&c->meta, nw::kMetaBytes) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
         nw_ctx_destroy(c);
         return NW_ERR_HIP;
@@ -174,6 +180,8 @@ void nw_ctx_destroy(nw_ctx *c) {
     (void)hipSetDevice(c->device);
     if (c->gran) (void)hipFree(c->gran);
     if (c->rowpack) (void)hipFree(c->rowpack);
+    if (c->prof) (void)hipFree(c->prof);
+    if (c->meta) (void)hipFree(c->meta);
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->ctrl) (void)hipFree(c->ctrl);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -220,6 +228,19 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
     NW_HIP_TRY(hipMemsetAsync(c->ctrl, 0, 16, (hipStream_t)stream));
     const uint8_t *s2u = n2 > 0 ? (const uint8_t *)d_s2 : (const uint8_t *)c->ctrl;
     if (nw::launch_rowpack(s2u, n2, 0, c->rowpack, qlen, stream) != hipSuccess) return NW_ERR_HIP;
+    // Query profiles when every substitution score minus GAP fits int8 (the
+    // kernel falls back to compares on the device when s1 holds more than
+    // kMaxProf distinct characters).
+    const bool prof_ok = fits_i8(p->match - p->gap) && fits_i8(p->mismatch - p->gap) &&
+                         !(p->flags & NW_FLAG_NO_PROFILE);
+    if (prof_ok) {
+        if ((st = grow(&c->prof, &c->prof_cap, (size_t)qlen * 16 * nw::kMaxProf, false)) != NW_OK)
+            return st;
+        const uint8_t *s1u = n1 > 0 ? (const uint8_t *)d_s1 : (const uint8_t *)c->ctrl;
+        if (nw::launch_profiles(s1u, n1, s2u, n2, 0, p->match, p->mismatch, p->gap, c->meta,
+                                c->prof, qlen, stream) != hipSuccess)
+            return NW_ERR_HIP;
+    }
 
     nw::FillArgs a;
     std::memset(&a, 0, sizeof a);
@@ -241,6 +262,10 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
     a.halo_out = band ? band->halo_out : nullptr;
     a.halo_tag = band ? band->tag : 0u;
     a.scratch = c->scratch;
+    a.prof = prof_ok ? c->prof : nullptr;
+    a.prof_stride = qlen;
+    a.charmap = c->meta;
+    a.nprof = (const uint32_t *)(c->meta + 256 + nw::kMaxProf);
     a.trace = c->trace;
     a.match = p->match;
     a.mismatch = p->mismatch;

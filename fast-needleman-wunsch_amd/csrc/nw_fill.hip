@@ -52,6 +52,10 @@ namespace nw {
 // s_memrealtime runs at 100 MHz on gfx9: 20 s watchdog for every bounded spin.
 constexpr uint64_t kTimeoutTicks = 100000000ull * 20ull;
 constexpr int32_t kDone = 0x7FFFFFFF;  // counter value: "no more waiting on me"
+constexpr int kStoreWaves = 2;         // store waves per strip workgroup
+#ifndef NW_BCAP
+#define NW_BCAP 0  // max older stores a store wave keeps in flight (0: no cap)
+#endif
 
 template <int C> struct Vec;
 template <> struct Vec<1> { typedef int32_t T; };
@@ -86,7 +90,12 @@ struct Lay {
     static constexpr int kRing = R * kSlot;          // ring bytes
     static constexpr int kFeed = kRing;              // byte offset of the feed buffers
     static constexpr int kCtl = kFeed + 2 * kWave * 4;
-    static constexpr int kBytes = kCtl + 16;         // [0] steps written, [1] rows read, [2] strip
+    // counters: [0] steps written, [1 + b] rows read by store wave b, [3] strip
+    static constexpr int kBytes = kCtl + 16;
+    // compute wave: check ring space every kChk steps, publish progress every
+    // kPub steps (coarse only where the slack R - 64 allows it)
+    static constexpr int kChk = R - 64 >= 48 ? 16 : 4;
+    static constexpr int kPub = R - 64 >= 48 ? 8 : 4;
 };
 
 __device__ __forceinline__ uint64_t gran_load(const uint64_t *p) {
@@ -107,23 +116,36 @@ __device__ __forceinline__ void ctr_store(int32_t *p, int32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// Slow path of the hand-off: re-poll until every lane's granule carries `tag`
-// (s_sleep between polls).  Bounded: gives up -- raising the error word -- after
-// kTimeoutTicks, or at once if another wave already raised it.  Returns the last
-// value read; the caller re-checks its tag.
-__device__ __noinline__ uint64_t wait_granules_slow(const uint64_t *g, uint32_t tag,
-                                                    uint32_t *ctrl) {
+// Slow path of the hand-off: re-poll the granules of one 64-row block until
+// those of chunk c (lanes 16c .. 16c+15) carry `tag` (s_sleep between polls).
+// Bounded: gives up -- raising the error word -- after kTimeoutTicks, or at once
+// if another wave already raised it.  Returns the last value read; the caller
+// re-checks its tag.
+__device__ __noinline__ uint64_t wait_chunk(const uint64_t *g, uint32_t tag, int c,
+                                            uint32_t *ctrl) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    const int lane = threadIdx.x & 63;
+    const bool in_chunk = (lane >> 4) == c;
     for (;;) {
         __builtin_amdgcn_s_sleep(1);
         const uint64_t v = gran_load(g);
-        if (__all((uint32_t)(v >> 32) == tag)) return v;
+        if (__all(!in_chunk || (uint32_t)(v >> 32) == tag)) return v;
         if (ctrl_load(ctrl + 1) != 0u) return v;
         if (__builtin_amdgcn_s_memrealtime() - t0 > kTimeoutTicks) {
-            if ((threadIdx.x & 63) == 0) atomicCAS(ctrl + 1, 0u, 1u);
+            if (lane == 0) atomicCAS(ctrl + 1, 0u, 1u);
             return v;
         }
     }
+}
+
+// Leading 16-row chunks of a block whose granules all carry `tag` (0 .. 4).
+__device__ __forceinline__ int chunks_ready(uint64_t v, uint32_t tag) {
+    const uint64_t ok = __ballot((uint32_t)(v >> 32) == tag);
+    int n = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+        if (n == c && ((ok >> (16 * c)) & 0xFFFFull) == 0xFFFFull) n = c + 1;
+    return n;
 }
 
 // Bounded spin until the LDS counter *p reaches `need`; returns the value seen
@@ -140,6 +162,19 @@ __device__ __noinline__ int32_t wait_counter(const int32_t *p, int32_t need, uin
         }
         __builtin_amdgcn_s_sleep(1);
     }
+}
+
+// Rows every store wave has read out of the ring (each publishes the start of
+// its next batch; all rows below the smallest are out).
+__device__ __forceinline__ int32_t rows_read(const int32_t *ctr) {
+    int32_t v = ctr_load(ctr + 1);
+#pragma unroll
+    for (int b = 1; b < kStoreWaves; ++b) v = min(v, ctr_load(ctr + 1 + b));
+    return v;
+}
+__device__ __forceinline__ void wait_rows_read(const int32_t *ctr, int32_t need, uint32_t *ctrl) {
+#pragma unroll
+    for (int b = 0; b < kStoreWaves; ++b) (void)wait_counter(ctr + 1 + b, need, ctrl);
 }
 
 // Row characters of local iteration j (steps 64j .. 64j+63): lane l needs the
@@ -161,24 +196,29 @@ __device__ __forceinline__ void static_for(F &&f) {
     }
 }
 
-// diag' + s'(a, b) for one cell: byte QB of the row-character word is compared
-// with byte KB of the lane's packed column characters (reference match test:
-// raw byte equality, serial.cpp:23-24), then
-//   UNIT (match - mismatch == 1, the reference default):  d = diag' + mm' + [a == b]
-//   general:                                               d = diag' + (a == b ? ms' : mm')
-// (ms' / mm' have GAP pre-subtracted, because diag' = t + GAP.)  One asm
-// statement per cell so hipcc keeps the compare next to its use.
-template <int QB, int KB, bool UNIT>
+// How a cell's substitution score is formed.
+//   SUB_PROF : query profile -- the row word holds s(a_k, b) - GAP per row as
+//              int8 (one profile per distinct column character, nw_profile);
+//              d = diag' + sext(byte):  ONE v_add_u32_sdwa, no compare
+//   SUB_UNIT : match - mismatch == 1: d = diag' + mm' + [a == b]
+//              (v_cmp_eq_u32_sdwa -> vcc -> v_addc)
+//   SUB_GEN  : d = diag' + (a == b ? ms' : mm')  (v_cmp -> vcc -> v_cndmask, add)
+// The compare forms test raw byte equality, the reference's match test
+// (serial.cpp:23-24); ms' / mm' / the profile bytes have GAP pre-subtracted
+// because diag' = t + GAP.  On a lone gfx950 wave the vcc round trip costs
+// ~15 cycles per cell, which is why the profile form exists.
+enum Sub { SUB_PROF = 0, SUB_UNIT = 1, SUB_GEN = 2 };
+
+template <int QB, int KB, int MODE>
 __device__ __forceinline__ int32_t diag_plus_sub(uint32_t pk, uint32_t apk, int32_t diag,
                                                  int32_t msp, int32_t mmp) {
     int32_t d;
-#ifdef NW_DBG_NOCMP
-    if (true) {  // timing only: wrong scores, no VCC traffic
-        d = diag + mmp + (int32_t)__builtin_amdgcn_ubfe(pk ^ apk, 8 * QB + KB, 1);
-        return d;
-    }
-#endif
-    if constexpr (UNIT) {
+    if constexpr (MODE == SUB_PROF) {
+        asm("v_add_u32_sdwa %0, %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD "
+            "src0_sel:DWORD src1_sel:BYTE_%c3"
+            : "=v"(d)
+            : "v"(diag), "v"(pk), "i"(QB));
+    } else if constexpr (MODE == SUB_UNIT) {
         asm volatile(
             "v_cmp_eq_u32_sdwa vcc, %1, %2 src0_sel:BYTE_%c4 src1_sel:BYTE_%c5\n\t"
             "v_addc_co_u32_e32 %0, vcc, %3, %6, vcc"
@@ -186,14 +226,14 @@ __device__ __forceinline__ int32_t diag_plus_sub(uint32_t pk, uint32_t apk, int3
             : "v"(pk), "v"(apk), "v"(diag), "i"(QB), "i"(KB), "v"(mmp)
             : "vcc");
     } else {
-        int32_t s;
+        int32_t sc;
         asm volatile(
             "v_cmp_eq_u32_sdwa vcc, %1, %2 src0_sel:BYTE_%c5 src1_sel:BYTE_%c6\n\t"
             "v_cndmask_b32_e32 %0, %3, %4, vcc"
-            : "=v"(s)
+            : "=v"(sc)
             : "v"(pk), "v"(apk), "v"(mmp), "v"(msp), "i"(QB), "i"(KB)
             : "vcc");
-        d = diag + s;
+        d = diag + sc;
     }
     return d;
 }
@@ -209,21 +249,45 @@ struct Lanes {
     int32_t cb;       // last value read of the store wave's row counter
 };
 
+// The feed of one iteration: the left neighbour's right column for rows
+// 64*it .. 64*it+63, published there in 16-row chunks.  `ready` leading chunks
+// were found published when the iteration started; before the group that
+// first reads chunk c >= ready, run_iter waits for it (wait_chunk) and writes
+// its 16 feed values.
+struct Feed {
+    const uint64_t *g;  // this lane's granule of the block (left neighbour's slot)
+    uint32_t tag;
+    int ready;
+    int32_t gap;
+    uint32_t nslow;
+    uint64_t wticks;
+    bool dead;
+    bool trace_pub;     // debug trace: stamp the publish of chunk 0 in this iteration
+    uint64_t tpub;
+};
+
+// Row words per lane and iteration: one per column of the lane in the profile
+// form (each column has its own character's profile), one in the compare forms.
+template <int C, int MODE>
+constexpr int npk() { return MODE == SUB_PROF ? C : 1; }
+
 // 64 wavefront steps of local iteration `it` (steps s = 64*it + u, u < 64) of
 // the compute wave.  Step s: compute row s - l on every lane l, write the
 // results to ring slot s mod R, shift the strip's right column (lane 63's
-// column C-1, row s - 63) into outcol.  After steps 4g+3 the steps-written
-// counter is published; before each 4-step group the slots it overwrites are
-// checked free (rows read by the store wave; the counter value was read one
-// group earlier, so its LDS latency is hidden).
-//   pk   : row-character words of this iteration (load_packs)
+// column C-1, row s - 63) into outcol.  Every kPub steps the steps-written
+// counter is published; every kChk steps the slots the next kChk overwrite are
+// checked free (rows read by the store wave; the counter value was read kChk
+// steps earlier, so its LDS latency is hidden).
+//   pk   : row words of this iteration (load_packs), [npk][4] x 16 rows each
 //   sb   : slot of step 64*it (= 64*it mod R)
-//   gp   : where block it-1's right column goes (published after step 62, when
-//          outcol holds rows 64*(it-1) .. 64*(it-1) + 63, lane l = row + l)
-template <int C, bool UNIT, bool RAMP>
-__device__ __forceinline__ void run_iter(char *__restrict__ lds, int it, const u32x4 (&pk)[4],
-                                         int32_t msp, int32_t mmp, int32_t gap, Lanes<C> &S,
-                                         int sb, uint64_t *gp, uint64_t tagw, uint32_t *ctrl,
+//   gp   : this lane's granule of block it-1 (the right column is published in
+//          16-row chunks, after steps 14, 30, 46, 62)
+//   F    : the feed of this iteration (chunks not yet published are waited for)
+template <int C, int MODE, bool RAMP>
+__device__ __forceinline__ void run_iter(char *__restrict__ lds, int it,
+                                         const u32x4 (&pk)[npk<C, MODE>()][4], int32_t msp,
+                                         int32_t mmp, int32_t gap, Lanes<C> &S, int sb,
+                                         uint64_t *gp, uint64_t tagw, uint32_t *ctrl, Feed &F,
                                          int lane) {
     typedef typename Vec<C>::T VT;
     typedef Lay<C> L;
@@ -233,19 +297,32 @@ __device__ __forceinline__ void run_iter(char *__restrict__ lds, int it, const u
     const int s0 = it * 64;
     static_for<0, 16>([&](auto gc) {
         constexpr int g = decltype(gc)::value;
-        // ring space for steps s0+4g .. s0+4g+3: their slots held anti-diagonals
-        // s - R, last needed by row s - R, so rows <= s0 + 4g + 3 - R must be read
-#ifndef NW_DBG_NOFLOW
-        {
-            const int32_t need = s0 + 4 * g + 4 - L::R;
-            if (__builtin_amdgcn_readfirstlane(S.cb) < need)
-                S.cb = wait_counter(ctr + 1, need, ctrl);
-            S.cb = ctr_load(ctr + 1);  // for the next group
+        // ring space for steps s0+4g .. s0+4g+kChk-1: their slots held
+        // anti-diagonals s - R, last needed by row s - R, so rows
+        // <= s0 + 4g + kChk - 1 - R must have been read
+        if constexpr ((4 * g) % L::kChk == 0) {
+            const int32_t need = s0 + 4 * g + L::kChk - L::R;
+            if (__builtin_amdgcn_readfirstlane(S.cb) < need) wait_rows_read(ctr, need, ctrl);
+            S.cb = rows_read(ctr);  // for the next check (kChk steps on)
         }
-#endif
+        // chunk (g+1)/4 is read by the feed load below: wait for it if it was
+        // not yet published when the iteration started
+        if constexpr ((g & 3) == 3 && g + 1 < 16) {
+            constexpr int c = (g + 1) >> 2;
+            if (F.ready <= c) {
+                const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
+                const uint64_t v = wait_chunk(F.g, F.tag, c, ctrl);
+                F.dead |= !__all((lane >> 4) != c || (uint32_t)(v >> 32) == F.tag);
+                F.nslow += 1;
+                F.wticks += __builtin_amdgcn_s_memrealtime() - w0;
+                if ((lane >> 4) == c)
+                    ((int32_t *)(lds + L::kFeed))[((it & 1) << 6) + lane] =
+                        (int32_t)(uint32_t)v + F.gap;
+                F.ready = c + 1;
+            }
+        }
         const int4 fcur = fq;
         if constexpr (g + 1 < 16) fq = feed4[g + 1];
-        const uint32_t pkw = pk[g >> 2][g & 3];
         static_for<0, 4>([&](auto qc) {
             constexpr int q = decltype(qc)::value;
             constexpr int u = 4 * g + q;
@@ -263,7 +340,8 @@ __device__ __forceinline__ void run_iter(char *__restrict__ lds, int it, const u
             VT tv;
             static_for<0, C>([&](auto kc) {
                 constexpr int k = decltype(kc)::value;
-                const int32_t d = diag_plus_sub<q, k, UNIT>(pkw, S.apk, diag, msp, mmp);
+                const uint32_t pkw = pk[MODE == SUB_PROF ? k : 0][g >> 2][g & 3];
+                const int32_t d = diag_plus_sub<q, k, MODE>(pkw, S.apk, diag, msp, mmp);
                 int32_t t = max(max(d, S.u[k]), left);  // max(diag+s, up+GAP, left+GAP)
                 diag = S.u[k];
                 if constexpr (RAMP) {
@@ -282,18 +360,24 @@ __device__ __forceinline__ void run_iter(char *__restrict__ lds, int it, const u
             *(VT *)(lds + slot * L::kSlot + lane * (4 * C)) = tv;
             S.outcol = __builtin_amdgcn_update_dpp(comp<C>(tv, C - 1), S.outcol,
                                                    0x130 /*wave_shl:1*/, 0xF, 0xF, false);
-            if constexpr (u == 62) gran_store(gp, tagw | (uint32_t)S.outcol);
-#ifndef NW_DBG_NOCTRA
-            if constexpr (q == 3) ctr_store(ctr, s0 + u + 1);  // steps written
-#endif
+            // after step 14 + 16c outcol's lanes 48..63 hold rows 64(it-1) + 16c + 0..15
+            // of the right column: publish that chunk (lane l -> row 64(it-1) + l - 48 + 16c)
+            if constexpr ((u & 15) == 14) {
+                if (lane >= 48) gran_store(gp + (16 * (u >> 4) - 48), tagw | (uint32_t)S.outcol);
+                if constexpr (u == 14) {
+                    if (F.trace_pub) F.tpub = __builtin_amdgcn_s_memrealtime();
+                }
+            }
+            if constexpr ((u + 1) % L::kPub == 0) ctr_store(ctr, s0 + u + 1);  // steps written
         });
     });
 }
 
 // The compute wave on strip p.
-template <int C, bool UNIT>
+template <int C, int MODE>
 __device__ void compute_strip(const FillArgs &A, char *__restrict__ lds, int p, int lane) {
     typedef Lay<C> L;
+    constexpr int NPK = npk<C, MODE>();
     const int32_t gap = A.gap;
     const int32_t msp = A.match - gap, mmp = A.mismatch - gap;
     const int64_t c0 = (int64_t)p * (64 * C);
@@ -351,67 +435,101 @@ __device__ void compute_strip(const FillArgs &A, char *__restrict__ lds, int p, 
     const int lastb = nblocks - 1;
     uint64_t *gscr = (uint64_t *)(A.scratch + (int64_t)blockIdx.x * kScratchWords) + lane;
 
-    // Prefetch pipeline: the left neighbour's granules (feed) and the
-    // row-character packs are loaded two iterations ahead into 3-deep register
-    // rings, so no wait for a load ever falls inside the steps.  Buffer =
-    // issue iteration mod 3; all loads unconditional (clamped indices).
-    uint64_t gb[3];
-    u32x4 pkb[3][4];
-    gb[0] = gran_load(gin);                                  // block 0, for iteration 0
-    gb[1] = gran_load(gin + (int64_t)min(1, lastb) * 64);    // block 1, for iteration 1
-    gb[2] = 0;
-    load_packs((const u32x4 *)A.rowpack, 0, lane, pkb[0]);
-    load_packs((const u32x4 *)A.rowpack, 1, lane, pkb[1]);
+    // Row words: the raw s2 bytes (compare forms), or per column k the profile
+    // of the lane's character a_k (profile form; nw_profile).
+    const u32x4 *pkp[NPK];
+    if constexpr (MODE == SUB_PROF) {
+#pragma unroll
+        for (int k = 0; k < C; ++k) {
+            const uint32_t m = min((uint32_t)A.charmap[(S.apk >> (8 * k)) & 255u], kMaxProf - 1u);
+            pkp[k] = (const u32x4 *)A.prof + (int64_t)m * A.prof_stride;
+        }
+    } else {
+        pkp[0] = (const u32x4 *)A.rowpack;
+    }
+    // Prefetch pipeline: the left neighbour's granules (feed) and the row words
+    // are loaded PD iterations ahead into (PD+1)-deep register rings, so no wait
+    // for a load falls inside the steps (PD = 2; 1 when four profile words per
+    // iteration would not fit in registers).  Buffer = iteration mod NB; all
+    // loads unconditional (clamped indices).
+    constexpr int NB = NPK >= 4 ? 2 : 3, PD = NB - 1;
+    uint64_t gb[NB];
+    u32x4 pkb[NB][NPK][4];
+#pragma unroll
+    for (int i = 0; i < PD; ++i) {
+        gb[i] = gran_load(gin + (int64_t)min(i, lastb) * 64);  // block i, for iteration i
+#pragma unroll
+        for (int k = 0; k < NPK; ++k) load_packs(pkp[k], i, lane, pkb[i][k]);
+    }
 
-    uint32_t nslow = 0;
-    uint64_t wticks = 0;
+    Feed F;
+    F.tag = tag_in;
+    F.gap = gap;
+    F.nslow = 0;
+    F.wticks = 0;
+    F.dead = dead;  // (a halo wait may already have given up)
     const uint64_t tstart = __builtin_amdgcn_s_memrealtime();
     const uint64_t cstart = __builtin_amdgcn_s_memtime();
     uint64_t tq1 = 0, tmid = 0;  // trace: times iterations nblocks/4 and nblocks/2 started
+    uint64_t tpub = 0, tsee = 0, twait = 0;  // trace: publish / see / wait start, block nblocks/2 chunk 0
+    F.trace_pub = false;
+    F.tpub = 0;
 
     // Iteration it: feed for block it (consumes buffer it % 3), prefetch for it+2
     // (into buffer (it+2) % 3), 64 steps, block it-1's right column published.
     // A watchdog trip marks the strip dead; it is abandoned at the boundary.
     auto iter = [&](int it, auto cons_c, auto ramp_c) {
-        constexpr int CONS = decltype(cons_c)::value;  // it % 3
-        constexpr int ISS = (CONS + 2) % 3;            // (it + 2) % 3
+        constexpr int CONS = decltype(cons_c)::value;  // it % NB
+        constexpr int ISS = (CONS + PD) % NB;          // (it + PD) % NB
         constexpr bool RAMP = decltype(ramp_c)::value;
         if (A.trace != nullptr) {
             if (it == nblocks / 4) tq1 = __builtin_amdgcn_s_memrealtime();
             if (it == nblocks / 2) tmid = __builtin_amdgcn_s_memrealtime();
+            F.trace_pub = it == nblocks / 2 + 1;
         }
         {
             int32_t fvv = kNeg;
+            F.ready = 4;
             if (has_left && it < nblocks) {
-                uint64_t gv = gb[CONS];  // block it, loaded two iterations ago
-                if (!__all((uint32_t)(gv >> 32) == tag_in)) {
+                uint64_t gv = gb[CONS];  // block it, loaded PD iterations ago
+                F.g = gin + (int64_t)it * 64;
+                F.ready = chunks_ready(gv, tag_in);
+                if (F.ready == 0) {  // chunk 0 is needed right away
                     const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
-                    gv = wait_granules_slow(gin + (int64_t)it * 64, tag_in, A.ctrl);
-                    dead = !__all((uint32_t)(gv >> 32) == tag_in);
-                    nslow += 1;
-                    wticks += __builtin_amdgcn_s_memrealtime() - w0;
+                    if (A.trace != nullptr && it == nblocks / 2) twait = w0;
+                    gv = wait_chunk(F.g, tag_in, 0, A.ctrl);
+                    F.dead |= !__all((lane >> 4) != 0 || (uint32_t)(gv >> 32) == tag_in);
+                    F.nslow += 1;
+                    F.wticks += __builtin_amdgcn_s_memrealtime() - w0;
+                    F.ready = max(1, chunks_ready(gv, tag_in));
                 }
                 fvv = (int32_t)(uint32_t)gv + gap;
+                if (A.trace != nullptr && it == nblocks / 2) tsee = __builtin_amdgcn_s_memrealtime();
             }
             ((int32_t *)(lds + L::kFeed))[((it & 1) << 6) + lane] = fvv;
         }
-        gb[ISS] = gran_load(gin + (int64_t)min(it + 2, lastb) * 64);
-        load_packs((const u32x4 *)A.rowpack, it + 2, lane, pkb[ISS]);
+        gb[ISS] = gran_load(gin + (int64_t)min(it + PD, lastb) * 64);
+#pragma unroll
+        for (int k = 0; k < NPK; ++k) load_packs(pkp[k], it + PD, lane, pkb[ISS][k]);
         const int b = it - 1;  // block whose right column this iteration publishes
         uint64_t *gp = (b >= 0 && b < nblocks) ? gout + (int64_t)b * 64 + lane : gscr;
         const int sb = __builtin_amdgcn_readfirstlane((int)(((uint32_t)it * 64u) % (uint32_t)L::R));
-        run_iter<C, UNIT, RAMP>(lds, it, pkb[CONS], msp, mmp, gap, S, sb, gp, tagw, A.ctrl, lane);
+        run_iter<C, MODE, RAMP>(lds, it, pkb[CONS], msp, mmp, gap, S, sb, gp, tagw, A.ctrl, F,
+                                lane);
+        dead = F.dead;
     };
     // iteration 0 ramps the wavefront in (lanes above row 1 hold row 0); row
     // 64*nblocks - 1 completes (lane 63) at step 64*nblocks + 62, iteration nblocks
     const int nit = nblocks + 1;
     iter(0, std::integral_constant<int, 0>{}, std::true_type{});
-    for (int it = 1; it < nit && !dead; it += 3) {
-        iter(it, std::integral_constant<int, 1>{}, std::false_type{});
+    for (int it = 1; it < nit && !dead; it += NB) {
+        iter(it, std::integral_constant<int, 1 % NB>{}, std::false_type{});
         if (it + 1 >= nit || dead) break;
-        iter(it + 1, std::integral_constant<int, 2>{}, std::false_type{});
-        if (it + 2 >= nit || dead) break;
-        iter(it + 2, std::integral_constant<int, 0>{}, std::false_type{});
+        iter(it + 1, std::integral_constant<int, 2 % NB>{}, std::false_type{});
+        if constexpr (NB == 3) {
+            if (it + 2 >= nit || dead) break;
+            iter(it + 2, std::integral_constant<int, 0>{}, std::false_type{});
+        }
     }
     // every row is in the ring (or the strip is abandoned): release the store wave
     ctr_store(ctr, kDone);
@@ -419,12 +537,15 @@ __device__ void compute_strip(const FillArgs &A, char *__restrict__ lds, int p, 
         uint64_t *tr = A.trace + (int64_t)p * kTraceWords;
         tr[0] = tstart;
         tr[1] = __builtin_amdgcn_s_memrealtime();
-        tr[2] = nslow;
-        tr[3] = wticks;
+        tr[2] = F.nslow;
+        tr[3] = F.wticks;
         tr[4] = tq1;
         tr[5] = tmid;
         tr[6] = cstart;                          // shader clock (s_memtime)
         tr[7] = __builtin_amdgcn_s_memtime();
+        tr[8] = F.tpub;
+        tr[9] = tsee;
+        tr[10] = twait;
     }
 }
 
@@ -433,10 +554,13 @@ __device__ void compute_strip(const FillArgs &A, char *__restrict__ lds, int p, 
 // two rows of a C = 2 strip): B-lane l takes row f + l / (16C), columns
 // 4 * (l % (16C)) .. +3, i.e. the pieces of the NR compute lanes
 // a = NR * (l % (16C)) + m that wrote them, each in slot (row + a) mod R.
-// Rows go in batches of BATCH: wait until the compute wave has written them,
-// read the whole batch from the ring, store it, then release its slots.
+// Rows go in batches of BATCH, dealt round robin to the kStoreWaves store waves
+// (b = this wave): wait until the compute wave has written the batch, read it
+// from the ring, store it, then release its slots.  Under full HBM load one
+// store instruction holds its wave for ~190 cycles, which is why one compute
+// wave has several store waves.
 template <int C>
-__device__ void store_strip(const FillArgs &A, char *__restrict__ lds, int p, int lane) {
+__device__ void store_strip(const FillArgs &A, char *__restrict__ lds, int p, int lane, int b) {
     typedef typename Vec<C>::T VT;
     typedef Lay<C> L;
     constexpr int NR = 4 / C;                  // rows per store instruction
@@ -452,24 +576,22 @@ __device__ void store_strip(const FillArgs &A, char *__restrict__ lds, int p, in
     const bool col_ok = c0 + 4 * cq < A.pitch;  // the last strip may overhang the pitch
     const int64_t rowb = timing ? 0 : A.pitch * 4;
     char *scr = (char *)(A.scratch + (int64_t)blockIdx.x * kScratchWords);
-    char *rowp = timing ? scr : (char *)(A.table + c0);
+    const int32_t f0 = b * BATCH;
+    char *rowp = timing ? scr : (char *)(A.table + c0) + (int64_t)f0 * rowb;
     const uint32_t voff = (uint32_t)(ro * rowb) + (uint32_t)cq * 16u;
     uint32_t pa[NR];  // ring byte address of piece m of this lane's row
 #pragma unroll
     for (int m = 0; m < NR; ++m) {
         const int a = NR * cq + m;
-        pa[m] = (uint32_t)((ro + a) % L::R) * L::kSlot + (uint32_t)a * (4u * C);
+        pa[m] = (uint32_t)((f0 + ro + a) % L::R) * L::kSlot + (uint32_t)a * (4u * C);
     }
-    auto adv = [&](uint32_t x) {  // NR rows further down the ring
-        x += NR * L::kSlot;
+    auto adv = [&](uint32_t x, uint32_t rows) {  // `rows` (< R) rows further down the ring
+        x += rows * L::kSlot;
         return x >= kRingB ? x - kRingB : x;
     };
+    int32_t *mine = ctr + 1 + b;
     int32_t avail = 0;  // rows complete in the ring (steps written - 63)
-#ifdef NW_DBG_BFREE
-    ctr_store(ctr + 1, kDone);
-    return;
-#endif
-    for (int32_t f = 0; f < nrows; f += BATCH) {
+    for (int32_t f = f0; f < nrows; f += kStoreWaves * BATCH) {
         const int32_t want = min(f + BATCH, nrows);
         if (avail < want) {
             int32_t sa = __builtin_amdgcn_readfirstlane(ctr_load(ctr));
@@ -482,14 +604,18 @@ __device__ void store_strip(const FillArgs &A, char *__restrict__ lds, int p, in
 #pragma unroll
             for (int m = 0; m < NR; ++m) {
                 const VT x = *(const VT *)(lds + pa[m]);
-                pa[m] = adv(pa[m]);
+                pa[m] = adv(pa[m], NR);
 #pragma unroll
                 for (int k = 0; k < C; ++k) v[g][m * C + k] = (uint32_t)comp<C>(x, k);
             }
         }
-#ifdef NW_DBG_BNOSTORE
-        if (v[0][0] == 0x12345678u && v[NG - 1][3] == 0x9abcdefu) *(u32x4 *)scr = v[0];
-#else
+#pragma unroll
+        for (int m = 0; m < NR; ++m) pa[m] = adv(pa[m], (kStoreWaves - 1) * BATCH);  // skip the others'
+#if NW_BCAP > 0
+        // keep this CU's store queue short: the compute wave's hand-off polls
+        // wait behind it (vmcnt: vmcnt[3:0] | vmcnt[5:4] << 14, others maxed)
+        __builtin_amdgcn_s_waitcnt((NW_BCAP & 15) | (7 << 4) | (15 << 8) | ((NW_BCAP >> 4) << 14));
+#endif
         if (want - f == BATCH) {
 #pragma unroll
             for (int g = 0; g < NG; ++g)
@@ -500,17 +626,18 @@ __device__ void store_strip(const FillArgs &A, char *__restrict__ lds, int p, in
                 if (col_ok && f + g * NR + ro < nrows)
                     *(u32x4 *)(rowp + (int64_t)g * NR * rowb + voff) = v[g];
         }
-#endif
-        rowp += BATCH * rowb;
-        ctr_store(ctr + 1, want);  // rows read: their slots may be overwritten
+        rowp += kStoreWaves * BATCH * rowb;
+        ctr_store(mine, f + kStoreWaves * BATCH);  // my rows below are out of the ring
     }
-    ctr_store(ctr + 1, kDone);
+    ctr_store(mine, kDone);
     // Row band: hand this strip's columns of the last row (n2) to the next band.
     // The table stores are plain (write-back L2), so: drain them, write the XCD's
     // L2 back (agent release), re-read the row with sc1 loads, publish
     // system-scope granules (write-through; peer HBM over xGMI when the next
     // band lives on another GPU).
-    if (A.halo_out != nullptr && ctrl_load(A.ctrl + 1) == 0u) {
+    // (the store wave that stored row n2 does it)
+    if (A.halo_out != nullptr && ((nrows - 1) / BATCH) % kStoreWaves == b &&
+        ctrl_load(A.ctrl + 1) == 0u) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         const int32_t *last = A.table + A.n2 * A.pitch;
@@ -527,9 +654,10 @@ __device__ void store_strip(const FillArgs &A, char *__restrict__ lds, int p, in
     }
 }
 
-// Persistent grid of two-wave workgroups: wave 0 computes, wave 1 stores.
+// Persistent grid of workgroups of 1 + kStoreWaves waves: wave 0 computes,
+// the others store.
 template <int C, bool UNIT>
-__global__ __launch_bounds__(128) void nw_fill_strips(FillArgs A) {
+__global__ __launch_bounds__(64 * (1 + kStoreWaves)) void nw_fill_strips(FillArgs A) {
     typedef Lay<C> L;
     __shared__ __attribute__((aligned(16))) char lds[L::kBytes];
     int32_t *ctr = (int32_t *)(lds + L::kCtl);
@@ -537,17 +665,24 @@ __global__ __launch_bounds__(128) void nw_fill_strips(FillArgs A) {
     const int wave = threadIdx.x >> 6;
     for (;;) {
         if (threadIdx.x == 0) {
-            ctr[0] = 0;
-            ctr[1] = 0;
-            ctr[2] = (int32_t)atomicAdd(A.ctrl, 1u);
+            for (int b = 0; b < 1 + kStoreWaves; ++b) ctr[b] = 0;
+            ctr[3] = (int32_t)atomicAdd(A.ctrl, 1u);
         }
         __syncthreads();
-        const int p = __builtin_amdgcn_readfirstlane(ctr[2]);
+        const int p = __builtin_amdgcn_readfirstlane(ctr[3]);
         if (p >= A.nstrips) break;
-        if (wave == 0)
-            compute_strip<C, UNIT>(A, lds, p, lane);
-        else
-            store_strip<C>(A, lds, p, lane);
+        if (wave == 0) {
+            // profile form when the launch's profiles exist (nprof of them, built
+            // by nw_profile from the column characters), else the compares
+            const uint32_t np = __builtin_amdgcn_readfirstlane(ctrl_load(A.nprof));
+            if (A.prof != nullptr && np >= 1u && np <= kMaxProf)
+                compute_strip<C, SUB_PROF>(A, lds, p, lane);
+            else if (UNIT)
+                compute_strip<C, SUB_UNIT>(A, lds, p, lane);
+            else
+                compute_strip<C, SUB_GEN>(A, lds, p, lane);
+        } else
+            store_strip<C>(A, lds, p, lane, wave - 1);
         __syncthreads();  // the ring and counters are reused by the next strip
     }
 }
@@ -569,6 +704,83 @@ __global__ void nw_rowpack(const uint8_t *__restrict__ s2, int64_t n2, int64_t r
     q[idx] = v;
 }
 
+// Column-character map of a launch (one workgroup): which byte values occur in
+// s1, in increasing order -> charmap[c] = profile index (0xFF: absent),
+// chars[m] = the character of profile m (m < kMaxProf), *nprof = how many
+// distinct characters s1 holds.
+__global__ __launch_bounds__(1024) void nw_charmap(const uint8_t *__restrict__ s1, int64_t n1,
+                                                   uint8_t *__restrict__ charmap,
+                                                   uint8_t *__restrict__ chars,
+                                                   uint32_t *__restrict__ nprof) {
+    __shared__ uint32_t present[8];
+    __shared__ uint32_t before[8];
+    if (threadIdx.x < 8) present[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t mine[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int64_t i = threadIdx.x; i < n1; i += blockDim.x) {
+        const uint32_t c = s1[i];
+        mine[c >> 5] |= 1u << (c & 31);
+    }
+#pragma unroll
+    for (int w = 0; w < 8; ++w)
+        if (mine[w]) atomicOr(&present[w], mine[w]);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (int w = 0; w < 8; ++w) {
+            before[w] = acc;
+            acc += (uint32_t)__builtin_popcount(present[w]);
+        }
+        *nprof = acc;
+    }
+    __syncthreads();
+    if (threadIdx.x < 256) {
+        const uint32_t c = threadIdx.x, w = c >> 5, bit = 1u << (c & 31);
+        const uint32_t idx = before[w] + (uint32_t)__builtin_popcount(present[w] & (bit - 1u));
+        const bool here = (present[w] & bit) != 0u;
+        charmap[c] = here ? (uint8_t)min(idx, 255u) : (uint8_t)0xFF;
+        if (here && idx < kMaxProf) chars[idx] = (uint8_t)c;
+    }
+}
+
+// Query profiles (SUB_PROF): prof[m * qlen + idx] = 16 int8 of
+// s(chars[m], B[x + k]) - GAP, k < 16, x = idx - kQOff, B[y] = s2[row0 + y - 1]
+// for 1 <= y <= n2 (else 0) -- the rowpack16 layout with the substitution score
+// of column character chars[m] against every row already applied.
+__global__ void nw_profile(const uint8_t *__restrict__ s2, int64_t n2, int64_t row0,
+                           const uint8_t *__restrict__ chars, const uint32_t *__restrict__ nprof,
+                           int32_t match, int32_t mismatch, int32_t gap, u32x4 *__restrict__ prof,
+                           int64_t qlen) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t m = blockIdx.y;
+    if (idx >= qlen || m >= *nprof) return;
+    const uint32_t a = chars[m];
+    const int64_t x = idx - kQOff;
+    u32x4 v = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int64_t y = x + k;
+        const uint32_t b = (y >= 1 && y <= n2) ? (uint32_t)s2[row0 + y - 1] : 0u;
+        const uint32_t sc = (uint32_t)((a == b ? match : mismatch) - gap) & 255u;
+        v[k >> 2] |= sc << (8 * (k & 3));
+    }
+    prof[(int64_t)m * qlen + idx] = v;
+}
+
+int launch_profiles(const uint8_t *d_s1, int64_t n1, const uint8_t *d_s2, int64_t n2,
+                    int64_t row0, int32_t match, int32_t mismatch, int32_t gap, uint8_t *meta,
+                    void *d_prof, int64_t qlen, void *stream) {
+    uint8_t *charmap = meta, *chars = meta + 256;
+    uint32_t *nprof = (uint32_t *)(meta + 256 + kMaxProf);
+    hipLaunchKernelGGL(nw_charmap, dim3(1), dim3(1024), 0, (hipStream_t)stream, d_s1, n1, charmap,
+                       chars, nprof);
+    const int bs = 256;
+    const int64_t nb = (qlen + bs - 1) / bs;
+    hipLaunchKernelGGL(nw_profile, dim3((unsigned)nb, kMaxProf), dim3(bs), 0, (hipStream_t)stream,
+                       d_s2, n2, row0, chars, nprof, match, mismatch, gap, (u32x4 *)d_prof, qlen);
+    return (int)hipGetLastError();
+}
+
 // entries of 16 bytes: iteration j <= nblocks + 2 (prefetch of the last one)
 // reads up to index kQOff + 64 * (nblocks + 2) + 48
 int64_t rowpack_len(int32_t nblocks) { return kQOff + 64 * ((int64_t)nblocks + 3) + 16; }
@@ -585,9 +797,9 @@ int launch_rowpack(const uint8_t *d_s2, int64_t n2, int64_t row0, void *d_q, int
 template <int C>
 static void launch_c(const FillArgs &a, int grid, hipStream_t s) {
     if (a.match - a.mismatch == 1)
-        hipLaunchKernelGGL((nw_fill_strips<C, true>), dim3(grid), dim3(2 * kWave), 0, s, a);
+        hipLaunchKernelGGL((nw_fill_strips<C, true>), dim3(grid), dim3((1 + kStoreWaves) * kWave), 0, s, a);
     else
-        hipLaunchKernelGGL((nw_fill_strips<C, false>), dim3(grid), dim3(2 * kWave), 0, s, a);
+        hipLaunchKernelGGL((nw_fill_strips<C, false>), dim3(grid), dim3((1 + kStoreWaves) * kWave), 0, s, a);
 }
 
 int launch_fill(const FillArgs &a, int substrips, int grid, void *stream) {

@@ -10,7 +10,9 @@ constexpr int kQOff = 64;          // rowpack index offset (lane l reads index 4
 constexpr int32_t kNeg = -(1 << 29);  // "minus infinity" fed left of column 0
 constexpr int kScratchWords = kWave * kWave + 2 * kWave;  // per workgroup (16.5 KB)
 constexpr int kMaxSub = 4;        // max columns per lane (strip = 64 * C columns)
-constexpr int kTraceWords = 8;     // debug trace words per strip
+constexpr int kTraceWords = 16;    // debug trace words per strip
+constexpr uint32_t kMaxProf = 16;  // query profiles per launch (distinct column characters)
+constexpr int kMetaBytes = 256 + kMaxProf + 16;  // charmap[256], chars[kMaxProf], nprof
 
 // Everything one launch of the strip-sweep kernel needs.  Plain POD, passed by
 // value as the kernel argument.
@@ -36,6 +38,13 @@ struct FillArgs {
     uint32_t halo_tag;         // launch tag shared with the neighbouring bands (> 0)
     int32_t *scratch;          // per-workgroup dummy flush target: grid * kScratchWords int32
     uint64_t *trace;           // optional per-strip debug trace [nstrips][kTraceWords]
+    // Query profiles (NULL = compare form): kMaxProf profiles of prof_stride
+    // 16-byte entries (rowpack16 layout, int8 s(c, row) - GAP), the character
+    // map of s1 and the count, all written on the device by launch_profiles.
+    const void *prof;
+    int64_t prof_stride;
+    const uint8_t *charmap;
+    const uint32_t *nprof;
     int32_t match, mismatch, gap;
     int32_t flags;             // debug: bit0 = send table stores to the scratch tile (timing only)
 };
@@ -43,6 +52,9 @@ struct FillArgs {
 // Launch helpers implemented in nw_fill.hip.  Return hipError_t as int.
 int launch_rowpack(const uint8_t *d_s2, int64_t n2, int64_t row0, void *d_q, int64_t qlen,
                    void *stream);
+int launch_profiles(const uint8_t *d_s1, int64_t n1, const uint8_t *d_s2, int64_t n2,
+                    int64_t row0, int32_t match, int32_t mismatch, int32_t gap, uint8_t *meta,
+                    void *d_prof, int64_t qlen, void *stream);
 int launch_fill(const FillArgs &a, int substrips, int grid, void *stream);
 int lds_bytes(int substrips);
 int64_t rowpack_len(int32_t nblocks);  // 16-byte entries

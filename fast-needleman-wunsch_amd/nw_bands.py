@@ -39,12 +39,17 @@ def plan(n2: int, nbands: int):
     return [nwhip.band_layout(n2, nbands, r) for r in range(nbands)]
 
 
-def resident_waves(device: int = 0, substrips: int = 1) -> int:
-    """Persistent workers that fit on the device at once (LDS-bound: a 64-slot
-    anti-diagonal ring of 64*substrips int32 + the feed buffer, as nw::lds_bytes)."""
+# LDS ring slots per strip workgroup by columns per lane (nw_fill.hip, Lay<C>::R)
+RING_SLOTS = {1: 148, 2: 152, 4: 76}
+
+
+def resident_waves(device: int = 0, substrips: int = 2) -> int:
+    """Persistent strip workers (workgroups) that fit on the device at once
+    (LDS-bound: the ring of R slots x 64*C int32 + two feed buffers + counters,
+    as nw::lds_bytes)."""
     import torch
     cus = torch.cuda.get_device_properties(device).multi_processor_count
-    lds = (substrips * 64 * 64 + 128) * 4
+    lds = substrips * 64 * 4 * RING_SLOTS[substrips] + 2 * 64 * 4 + 16
     return cus * (LDS_PER_CU // lds)
 
 
@@ -54,7 +59,7 @@ class LocalBands:
     Each band gets at most 1/P of the resident workers so that all bands are
     co-resident (a band waiting for its halo never blocks its producer)."""
 
-    def __init__(self, n1: int, n2: int, nbands: int, device: int = 0, substrips: int = 1):
+    def __init__(self, n1: int, n2: int, nbands: int, device: int = 0, substrips: int = 2):
         import torch
         self.n1, self.n2, self.P, self.device = n1, n2, nbands, device
         self.substrips = substrips

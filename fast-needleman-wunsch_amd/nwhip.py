@@ -163,12 +163,16 @@ def _seq(s) -> np.ndarray:
     return np.ascontiguousarray(np.asarray(s, dtype=np.int8))
 
 
-def fill(s1, s2, scheme=(1, 0, -1), waves: int = 0, device: int = -1, substrips: int = 0):
+FLAG_TIMING_ONLY, FLAG_NO_PROFILE = 1, 2  # nw_params.flags (include/nw_hip.h)
+
+
+def fill(s1, s2, scheme=(1, 0, -1), waves: int = 0, device: int = -1, substrips: int = 0,
+         flags: int = 0):
     """Full table in the reference layout ((n2+1) x (n1+1) int32) + NwResult."""
     a, b = _seq(s1), _seq(s2)
     t = np.empty((b.size + 1, a.size + 1), dtype=np.int32)
     r = NwResult()
-    p = params(scheme, waves, device, substrips=substrips)
+    p = params(scheme, waves, device, flags=flags, substrips=substrips)
     st = lib().nw_fill(a.ctypes.data_as(_i8p), a.size, b.ctypes.data_as(_i8p), b.size,
                        ctypes.byref(p), t.ctypes.data_as(_i32p), ctypes.byref(r))
     if st != NW_OK:

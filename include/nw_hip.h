@@ -43,6 +43,12 @@ enum {
 
 enum { NW_MODE_NW = 0 };
 
+/* nw_params.flags (0 = normal fill) */
+enum {
+    NW_FLAG_TIMING_ONLY = 1, /* table stores go to a scratch tile (kernel timing only) */
+    NW_FLAG_NO_PROFILE = 2   /* substitution by byte compares instead of query profiles */
+};
+
 /* Runtime replacement for the compile-time constants of
  * src/common/needleman-wunsch.hpp:11-13 (MATCH 1, MISMATCH 0, GAP -1). */
 typedef struct nw_params {
@@ -52,7 +58,7 @@ typedef struct nw_params {
     int32_t mode;      /* NW_MODE_NW */
     int32_t waves;     /* persistent strip workers (waves; 0 = auto)     */
     int32_t device;    /* HIP device ordinal, -1 = current device         */
-    int32_t flags;     /* reserved, 0                                     */
+    int32_t flags;     /* NW_FLAG_* bits, 0 for a normal fill            */
     int32_t substrips; /* 64-column sub-strips per wave (1, 2 or 4); 0 = auto */
 } nw_params;
 

@@ -96,21 +96,44 @@ SHAPES = [(0, 0), (0, 1), (1, 0), (1, 1), (2, 3), (63, 63), (64, 64), (65, 65), 
 @pytest.mark.parametrize("shape", SHAPES)
 @pytest.mark.parametrize("alphabet", ["dna", "bytes"])
 @pytest.mark.parametrize("substrips", [1, 2, 4])
-def test_random_vs_oracle(shape, alphabet, substrips):
+@pytest.mark.parametrize("form", ["profile", "compare"])
+def test_random_vs_oracle(shape, alphabet, substrips, form):
+    """Both substitution forms: query profiles (default; the "bytes" alphabet has
+    more distinct column characters than profiles and falls back on the device)
+    and byte compares (NW_FLAG_NO_PROFILE)."""
     rng = np.random.default_rng(shape[0] * 7919 + shape[1] + (alphabet == "bytes"))
     lo, hi = (1, 5) if alphabet == "dna" else (-128, 128)
     s1 = rng.integers(lo, hi, shape[0]).astype(np.int8)
     s2 = rng.integers(lo, hi, shape[1]).astype(np.int8)
+    flags = nwhip.FLAG_NO_PROFILE if form == "compare" else 0
     for scheme in SCHEMES.values():
-        t, r = nwhip.fill(s1, s2, scheme, substrips=substrips)
+        t, r = nwhip.fill(s1, s2, scheme, substrips=substrips, flags=flags)
         assert r.substrips == substrips
         np.testing.assert_array_equal(t, oracle.fill(s1, s2, scheme),
-                                      err_msg=str((shape, scheme, substrips)))
+                                      err_msg=str((shape, scheme, substrips, form)))
 
 
-@pytest.mark.parametrize("scheme", [(3, -2, -2), (1, 1, -1), (0, -1, -3), (5, 0, 0), (2, -3, 1)])
+@pytest.mark.parametrize("ndistinct", [1, 2, 15, 16, 17, 40])
+def test_profile_count_boundary(ndistinct):
+    """Up to 16 distinct column characters use query profiles, more fall back to
+    compares inside the kernel; the table is the same either way.  Row characters
+    outside the column alphabet (never matching) are included."""
+    rng = np.random.default_rng(ndistinct)
+    alphabet = rng.choice(np.arange(-128, 128), ndistinct, replace=False)
+    s1 = rng.choice(alphabet, 900).astype(np.int8)
+    s1[:ndistinct] = alphabet  # every character present
+    s2 = rng.integers(-128, 128, 650).astype(np.int8)
+    s2[::3] = rng.choice(alphabet, s2[::3].size)
+    for scheme in [(1, 0, -1), (2, -1, -2), (7, -5, 3)]:
+        t, _ = nwhip.fill(s1, s2, scheme)
+        np.testing.assert_array_equal(t, oracle.fill(s1, s2, scheme), err_msg=str(scheme))
+
+
+@pytest.mark.parametrize("scheme", [(3, -2, -2), (1, 1, -1), (0, -1, -3), (5, 0, 0), (2, -3, 1),
+                                    (150, -10, -1), (-5, -200, 3), (4095, -4095, -4095)])
 def test_other_schemes_vs_oracle(scheme):
-    """Runtime scores beyond the reference's #defines (incl. gap 0 and a positive gap)."""
+    """Runtime scores beyond the reference's #defines (incl. gap 0, a positive gap,
+    and scores whose s - GAP leaves int8, which take the compare form)."""
     rng = np.random.default_rng(11)
     s1 = rng.integers(1, 5, 700).astype(np.int8)
     s2 = rng.integers(1, 5, 333).astype(np.int8)

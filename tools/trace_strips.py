@@ -23,7 +23,7 @@ s1 = torch.from_numpy(nwhip.synth(1, n)).cuda()
 s2 = torch.from_numpy(nwhip.synth(2, n)).cuda()
 tab = nwhip.Context.alloc_table(n, n)
 nstrips = (n + 1 + 63) // 64
-tr = torch.zeros(nstrips * 8, dtype=torch.int64, device="cuda")
+tr = torch.zeros(nstrips * 16, dtype=torch.int64, device="cuda")
 for w in [int(x) for x in args.waves.split(",")]:
     ctx.set_trace(None)
     r0 = ctx.fill(s1, s2, tab, waves=w, flags=args.flags, substrips=args.sub)
@@ -31,7 +31,7 @@ for w in [int(x) for x in args.waves.split(",")]:
     r = ctx.fill(s1, s2, tab, waves=w, flags=args.flags, substrips=args.sub)
     nstrips = r.strips
     ctx.set_trace(None)
-    t = tr[: nstrips * 8].view(nstrips, 8).cpu().numpy().astype(np.float64)
+    t = tr[: nstrips * 16].view(nstrips, 16).cpu().numpy().astype(np.float64)
     if args.save:
         np.save(f"{args.save}_w{w}_k{r.substrips}.npy", t)
     t0 = t[:, 0].min()
@@ -51,6 +51,17 @@ for w in [int(x) for x in args.waves.split(",")]:
             print(f"  hop lag at {nm} (us): mean {hop.mean():.2f} p10 {pq[0]:.2f} med {pq[1]:.2f} p90 {pq[2]:.2f} "
                   f"p99 {np.percentile(hop, 99):.2f} max {hop.max():.1f}; "
                   f"first pass med {np.median(hop[:w]):.2f}; later med {np.median(later):.2f}")
+    # hand-off visibility: producer p-1 starts iteration nblocks/2+1 (publishes
+    # block nblocks/2 chunk 0 14 steps later) -> consumer p sees that chunk
+    ok = (t[1:, 9] > 0) & (t[:-1, 8] > 0)
+    vis = (t[1:, 9] - t[:-1, 8])[ok] / 100.0
+    waited = (t[1:, 10] > 0)[ok]
+    if vis.size:
+        pr = lambda a: f"p10 {np.percentile(a, 10):.2f} med {np.median(a):.2f} p90 {np.percentile(a, 90):.2f} (n={a.size})"
+        print(f"  block mid chunk 0: consumer saw it - producer published (us): all {pr(vis)}")
+        if waited.any():
+            print(f"     consumers that waited for it: {pr(vis[waited])}; waited from publish-x: "
+                  f"{pr(((t[1:, 10] - t[:-1, 8])[ok][waited]) / 100.0)}")
     busy = (dur - t[:, 3] / 100.0).sum()
     print(f"  sum(strip time - wait) / (waves * span) = {busy / (r.waves * en.max()):.3f}; "
           f"sum(wait) / (waves*span) = {t[:, 3].sum() / 100.0 / (r.waves * en.max()):.3f}")
