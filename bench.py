@@ -35,7 +35,9 @@ def parse():
     ap.add_argument("--n", type=int, default=262144, help="sequence length (N x N table)")
     ap.add_argument("--scheme", default="1,0,-1", help="match,mismatch,gap")
     ap.add_argument("--waves", type=int, default=0)
-    ap.add_argument("--substrips", type=int, default=0, help="64-col sub-strips per wave (0 = auto)")
+    ap.add_argument("--substrips", type=int, default=0, help="columns per lane C (0 = auto)")
+    ap.add_argument("--strip-waves", type=int, default=0,
+                    help="chained compute waves per strip NC (0 = auto)")
     ap.add_argument("--band-rows", type=int, default=65536,
                     help="N>1: rows per GPU band (weak scaling; N=8 -> 512k x 512k, config 4)")
     ap.add_argument("--band-cols", type=int, default=524288, help="N>1: table columns n1")
@@ -117,7 +119,8 @@ def run_single(args):
     stream = torch.cuda.current_stream()
 
     for _ in range(args.warmup):
-        ctx.fill(s1, s2, tab, scheme, waves=args.waves, sync=False, substrips=args.substrips)
+        ctx.fill(s1, s2, tab, scheme, waves=args.waves, sync=False, substrips=args.substrips,
+                 strip_waves=args.strip_waves)
     torch.cuda.synchronize()
 
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -126,7 +129,8 @@ def run_single(args):
     t0 = time.perf_counter()
     for e0, e1 in evs:
         e0.record(stream)
-        ctx.fill(s1, s2, tab, scheme, waves=args.waves, sync=False, substrips=args.substrips)
+        ctx.fill(s1, s2, tab, scheme, waves=args.waves, sync=False, substrips=args.substrips,
+                 strip_waves=args.strip_waves)
         e1.record(stream)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0

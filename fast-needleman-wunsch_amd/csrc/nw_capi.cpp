@@ -24,9 +24,7 @@ struct nw_ctx {
     size_t gran_cap = 0;  // bytes
     void *rowpack = nullptr;
     size_t rowpack_cap = 0;
-    void *prof = nullptr;      // query profiles (kMaxProf x rowpack entries)
-    size_t prof_cap = 0;
-    uint8_t *meta = nullptr;   // charmap / chars / nprof (nw::kMetaBytes)
+    uint8_t *meta = nullptr;   // charmap / nprof (nw::kMetaBytes)
     int32_t *scratch = nullptr;
     size_t scratch_cap = 0;
     uint32_t *ctrl = nullptr;  // 4 words
@@ -35,6 +33,7 @@ struct nw_ctx {
     int last_waves = 0;
     int last_strips = 0;
     int last_sub = 0;
+    int last_nc = 0;
     uint64_t *trace = nullptr;  // debug: per-strip timestamps (nw_debug_set_trace)
 };
 
@@ -66,21 +65,26 @@ int grow(void **p, size_t *cap, size_t need, bool zero) {
 
 struct Shape {
     int64_t nRows, nCols, nstrips, nblocks, waves, M, gstride;
-    int32_t K;
+    int32_t K, NC;
 };
 
-constexpr int kDefaultSub = 2;
+constexpr int kDefaultSub = 2;         // columns per lane
+constexpr int kDefaultStripWaves = 2;  // chained compute waves per strip
 constexpr int kLdsPerCU = 160 * 1024;
 
-Shape make_shape(int64_t n1, int64_t n2, int32_t waves_req, int32_t sub_req, int cus) {
+// col0: first swept column (1 when the table's column 1 starts a 256-byte line)
+Shape make_shape(int64_t n1, int64_t n2, int32_t waves_req, int32_t sub_req, int32_t nc_req,
+                 int cus, int64_t col0) {
     Shape s;
     s.K = sub_req > 0 ? sub_req : kDefaultSub;
+    s.NC = nc_req > 0 ? nc_req : (sub_req > 0 ? (s.K == 1 ? 4 : s.K == 2 ? 2 : 1) : kDefaultStripWaves);
     s.nRows = n2 + 1;
     s.nCols = n1 + 1;
-    s.nstrips = (s.nCols + nw::kWave * s.K - 1) / (nw::kWave * s.K);
+    const int64_t width = (int64_t)nw::kWave * s.K * s.NC;
+    s.nstrips = std::max<int64_t>(1, (s.nCols - col0 + width - 1) / width);
     s.nblocks = (s.nRows + nw::kWave - 1) / nw::kWave;
-    // one single-wave workgroup per LDS ring set; as many as fit in a CU's LDS
-    const int64_t per_cu = std::max(1, kLdsPerCU / nw::lds_bytes(s.K));
+    // one strip workgroup per LDS ring set; as many as fit in a CU's LDS
+    const int64_t per_cu = std::max(1, kLdsPerCU / nw::lds_bytes(s.K, s.NC));
     int64_t w = waves_req > 0 ? waves_req : per_cu * cus;
     s.waves = std::max<int64_t>(1, std::min<int64_t>(w, s.nstrips));
     // Strip p publishes into slot p % M.  When strip p is claimed, every strip
@@ -96,6 +100,8 @@ bool valid_params(const nw_params *p) {
     if (!p) return false;
     if (p->mode != NW_MODE_NW) return false;
     if (p->substrips != 0 && p->substrips != 1 && p->substrips != 2 && p->substrips != 4) return false;
+    if (p->strip_waves != 0 && p->strip_waves != 1 && p->strip_waves != 2 && p->strip_waves != 4)
+        return false;
     // keep every intermediate far from int32 overflow (|score| < 2^29)
     const int32_t lim = 1 << 12;
     return std::abs(p->match) < lim && std::abs(p->mismatch) < lim && std::abs(p->gap) < lim;
@@ -135,14 +141,24 @@ const char *nw_version(void) {
     return buf;
 }
 
-int64_t nw_table_pitch(int64_t n1) { return round_up(n1 + 1, nw::kWave); }
+// nCols = n1 + 1 rounded up to 64, with >= 3 columns of slack after column n1 so
+// that the 16-byte store holding column n1 stays inside the row when the strips
+// start at column 1 (nw_table_offset)
+int64_t nw_table_pitch(int64_t n1) { return round_up(n1 + 4, nw::kWave); }
 
 int64_t nw_table_bytes(int64_t n1, int64_t n2) {
     return round_up(n2 + 1, nw::kWave) * nw_table_pitch(n1) * (int64_t)sizeof(int32_t);
 }
 
+int64_t nw_table_offset(void) { return nw::kWave - 1; }
+
+int64_t nw_strip_lds_bytes(int32_t substrips, int32_t strip_waves) {
+    if (!nw::shape_ok(substrips, strip_waves)) return -1;
+    return nw::lds_bytes(substrips, strip_waves);
+}
+
 int64_t nw_ctx_workspace_bytes(int64_t n1, int64_t n2, int32_t waves) {
-    Shape s = make_shape(n1, n2, waves, 0, 256);
+    Shape s = make_shape(n1, n2, waves, 0, 0, 256, 1);
     return s.M * s.gstride * 8 + nw::rowpack_len((int32_t)s.nblocks) * 16 +
            s.waves * nw::kScratchWords * 4 + 16;
 }
@@ -165,7 +181,7 @@ int nw_ctx_create(int device, nw_ctx **out) {
     nw_ctx *c = new nw_ctx();
     c->device = device;
     c->cus = prop.multiProcessorCount;
-    if (hipMalloc(&c->ctrl, 16) != hipSuccess || hipMemset(c->ctrl, 0, 16) != hipSuccess ||
+    if (hipMalloc(&c->ctrl, 32) != hipSuccess || hipMemset(c->ctrl, 0, 32) != hipSuccess ||
         hipMalloc(&c->meta, nw::kMetaBytes) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
         nw_ctx_destroy(c);
@@ -180,7 +196,6 @@ void nw_ctx_destroy(nw_ctx *c) {
     (void)hipSetDevice(c->device);
     if (c->gran) (void)hipFree(c->gran);
     if (c->rowpack) (void)hipFree(c->rowpack);
-    if (c->prof) (void)hipFree(c->prof);
     if (c->meta) (void)hipFree(c->meta);
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->ctrl) (void)hipFree(c->ctrl);
@@ -195,15 +210,27 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
     if (!c || !d_t || n1 < 0 || n2 < 0 || n1 >= INT32_MAX || n2 >= INT32_MAX) return NW_ERR_ARG;
     if ((n1 > 0 && !d_s1) || (n2 > 0 && !d_s2)) return NW_ERR_ARG;
     if (!valid_params(p)) return NW_ERR_ARG;
-    if (pitch < nw_table_pitch(n1) || pitch % nw::kWave != 0) return NW_ERR_ARG;
-    if (((uintptr_t)d_t & 255u) != 0) return NW_ERR_ARG;
+    // any 64-multiple pitch that holds nCols = n1 + 1 (nw_table_pitch adds the
+    // slack that lets the strips start at column 1)
+    if (pitch < n1 + 1 || pitch % nw::kWave != 0) return NW_ERR_ARG;
+    // Strip origin: column 1 when the base is laid out so that column 1 starts a
+    // 256-byte line (nw_table_offset), which takes the boundary column 0 out of
+    // the sweep; column 0 for a 256-byte aligned base.  Anything else is refused.
+    int64_t col0;
+    if ((((uintptr_t)d_t + 4u) & 255u) == 0 && n1 >= 1 && pitch >= n1 + 4)
+        col0 = 1;
+    else if (((uintptr_t)d_t & 255u) == 0)
+        col0 = 0;
+    else
+        return NW_ERR_ARG;
     if (band) {
         if (band->tag == 0 || (((uintptr_t)band->halo_in | (uintptr_t)band->halo_out) & 7u) != 0)
             return NW_ERR_ARG;
         if (band->halo_out && (p->flags & 1)) return NW_ERR_ARG;  // needs the real last row
     }
     NW_HIP_TRY(hipSetDevice(c->device));
-    const Shape s = make_shape(n1, n2, p->waves, p->substrips, c->cus);
+    const Shape s = make_shape(n1, n2, p->waves, p->substrips, p->strip_waves, c->cus, col0);
+    if (!nw::shape_ok(s.K, s.NC)) return NW_ERR_ARG;
     if (s.nstrips > INT32_MAX / 2 || s.nblocks > INT32_MAX / 2) return NW_ERR_ARG;
 
     int st;
@@ -225,22 +252,17 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
                    (size_t)s.waves * nw::kScratchWords * 4, false)) != NW_OK)
         return st;
 
-    NW_HIP_TRY(hipMemsetAsync(c->ctrl, 0, 16, (hipStream_t)stream));
+    NW_HIP_TRY(hipMemsetAsync(c->ctrl, 0, 32, (hipStream_t)stream));
+    const uint8_t *s1u = n1 > 0 ? (const uint8_t *)d_s1 : (const uint8_t *)c->ctrl;
     const uint8_t *s2u = n2 > 0 ? (const uint8_t *)d_s2 : (const uint8_t *)c->ctrl;
-    if (nw::launch_rowpack(s2u, n2, 0, c->rowpack, qlen, stream) != hipSuccess) return NW_ERR_HIP;
-    // Query profiles when every substitution score minus GAP fits int8 (the
-    // kernel falls back to compares on the device when s1 holds more than
-    // kMaxProf distinct characters).
-    const bool prof_ok = fits_i8(p->match - p->gap) && fits_i8(p->mismatch - p->gap) &&
+    // v_perm score tables when every substitution score minus GAP fits int8
+    // (the kernel falls back to compares on the device when s1 holds more than
+    // kMaxPerm distinct characters).
+    const bool perm_ok = fits_i8(p->match - p->gap) && fits_i8(p->mismatch - p->gap) &&
                          !(p->flags & NW_FLAG_NO_PROFILE);
-    if (prof_ok) {
-        if ((st = grow(&c->prof, &c->prof_cap, (size_t)qlen * 16 * nw::kMaxProf, false)) != NW_OK)
-            return st;
-        const uint8_t *s1u = n1 > 0 ? (const uint8_t *)d_s1 : (const uint8_t *)c->ctrl;
-        if (nw::launch_profiles(s1u, n1, s2u, n2, 0, p->match, p->mismatch, p->gap, c->meta,
-                                c->prof, qlen, stream) != hipSuccess)
-            return NW_ERR_HIP;
-    }
+    if (nw::launch_rowpack(s1u, n1, s2u, n2, 0, perm_ok ? 1 : 0, c->meta, c->rowpack, qlen,
+                           stream) != hipSuccess)
+        return NW_ERR_HIP;
 
     nw::FillArgs a;
     std::memset(&a, 0, sizeof a);
@@ -251,6 +273,7 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
     a.n1 = n1;
     a.n2 = n2;
     a.row0 = 0;
+    a.col0 = col0;
     a.nstrips = (int32_t)s.nstrips;
     a.nblocks = (int32_t)s.nblocks;
     a.gran = c->gran;
@@ -262,20 +285,20 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
     a.halo_out = band ? band->halo_out : nullptr;
     a.halo_tag = band ? band->tag : 0u;
     a.scratch = c->scratch;
-    a.prof = prof_ok ? c->prof : nullptr;
-    a.prof_stride = qlen;
+    a.perm = perm_ok ? 1 : 0;
     a.charmap = c->meta;
-    a.nprof = (const uint32_t *)(c->meta + 256 + nw::kMaxProf);
+    a.nprof = (const uint32_t *)(c->meta + 256);
     a.trace = c->trace;
     a.match = p->match;
     a.mismatch = p->mismatch;
     a.gap = p->gap;
     a.flags = p->flags;
-    if (nw::launch_fill(a, s.K, (int)s.waves, stream) != hipSuccess) return NW_ERR_HIP;
+    if (nw::launch_fill(a, s.K, s.NC, (int)s.waves, stream) != hipSuccess) return NW_ERR_HIP;
     c->tagbase += (uint32_t)s.nstrips + 1u;
     c->last_waves = (int)s.waves;
     c->last_strips = (int)s.nstrips;
     c->last_sub = s.K;
+    c->last_nc = s.NC;
     return NW_OK;
 }
 
@@ -381,6 +404,7 @@ int nw_fill_device(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *d_s2
     out->strips = c->last_strips;
     out->waves = c->last_waves;
     out->substrips = c->last_sub;
+    out->strip_waves = c->last_nc;
     int32_t score = 0;
     NW_HIP_TRY(hipMemcpy(&score, d_t + n2 * pitch + n1, 4, hipMemcpyDeviceToHost));
     out->score = score;
@@ -414,8 +438,11 @@ int nw_fill(const int8_t *s1, int64_t n1, const int8_t *s2, int64_t n2, const nw
     nw_result r;
     std::memset(&r, 0, sizeof r);
     int st = NW_OK;
-    hipError_t e = hipMalloc(&d_t, (size_t)nw_table_bytes(n1, n2));
+    // column 1 on a 256-byte line: the allocation (256-byte aligned) + nw_table_offset
+    int32_t *d_alloc = nullptr;
+    hipError_t e = hipMalloc(&d_alloc, (size_t)nw_table_bytes(n1, n2) + 256);
     if (e != hipSuccess) return e == hipErrorOutOfMemory ? NW_ERR_OOM : NW_ERR_HIP;
+    d_t = d_alloc + (n1 >= 1 ? nw_table_offset() : 0);  // (no column 1 when n1 = 0)
     if (hipMalloc(&d_s1, (size_t)std::max<int64_t>(n1, 1)) != hipSuccess ||
         hipMalloc(&d_s2, (size_t)std::max<int64_t>(n2, 1)) != hipSuccess) {
         st = NW_ERR_OOM;
@@ -431,12 +458,22 @@ int nw_fill(const int8_t *s1, int64_t n1, const int8_t *s2, int64_t n2, const nw
                         hipMemcpyDeviceToHost) != hipSuccess)
             st = NW_ERR_HIP;
     }
-    (void)hipFree(d_t);
+    (void)hipFree(d_alloc);
     if (d_s1) (void)hipFree(d_s1);
     if (d_s2) (void)hipFree(d_s2);
     r.status = st;
     if (out) *out = r;
     return st;
+}
+
+// Debug hook (not part of the public ABI): the control words of the last launch
+// (ticket, error code, watchdog site / need / seen -- nw_fill.hip give_up).
+int nw_debug_ctrl(nw_ctx *c, uint32_t *out8) {
+    if (!c || !out8) return NW_ERR_ARG;
+    NW_HIP_TRY(hipSetDevice(c->device));
+    NW_HIP_TRY(hipDeviceSynchronize());
+    NW_HIP_TRY(hipMemcpy(out8, c->ctrl, 32, hipMemcpyDeviceToHost));
+    return NW_OK;
 }
 
 // Debug hook (not part of the public ABI): per-strip trace buffer, device memory

@@ -8,34 +8,47 @@
 //   t[0][j] = j*GAP, t[i][0] = i*GAP                              (serial.cpp:16-17)
 //
 // Decomposition (DESIGN.md section 4 has the full picture):
-//   * The table is cut into vertical STRIPS of 64*C columns.  Each strip is
-//     swept top to bottom by one workgroup of two waves:
-//       - the COMPUTE wave: lane l owns the C consecutive columns c0 + C*l + k
-//         and at step s computes row i = s - l for all of them -- an
-//         anti-diagonal wavefront across the lanes, a left-to-right chain of C
-//         cells inside each lane.  Per cell:
-//           d = diag' + s'(a, b)      v_cmp_eq_u32_sdwa (byte selects) + v_addc
+//   * Columns col0 .. n1 are cut into vertical STRIPS of NC*64*C columns (by
+//     default NC = 2 chained compute waves of C = 2 columns per lane: 256
+//     columns, one strip per CU at a time).  col0 = 1 when the table base is
+//     laid out so that column 1 starts a 256-byte line (nw_table_offset): then
+//     the boundary column 0 (t[i][0] = i*GAP) is not swept at all and an
+//     N x N table is exactly N/256 strips.  Each strip is swept top to bottom
+//     by one workgroup:
+//       - NC COMPUTE waves, wave j owning the strip's columns j*64C .. +64C-1.
+//         Lane l owns the C consecutive columns j*64C + C*l + k and at step s
+//         computes row i = s - l for all of them -- an anti-diagonal wavefront
+//         across the lanes, a left-to-right chain of C cells inside each lane.
+//         Per cell:
+//           d = diag' + s'(a, b)      v_add_u32_sdwa (a byte of a v_perm result)
 //           t = max3(d, up', left')   v_max3_i32
 //           u = t + GAP               v_add_u32   (u = what neighbours consume)
-//         up' is the lane's own register; left'/diag' of column k > 0 are the
-//         lane's own column k-1 (this step / last step).  Column 0 takes left'
-//         from lane l-1's column C-1 of the previous step (DPP wave_shr:1, whose
-//         "old" operand feeds lane 0 from the strip on the left) and diag' from
-//         what it received the step before.  Each step's C results go to an LDS
-//         ring indexed by ANTI-DIAGONAL (slot = step mod R, lane l at byte 4*C*l)
-//         with one conflict-free ds_write_b(32*C).  This wave issues no table
-//         stores: on gfx950 a vector store holds its wave for ~45-90 cycles.
-//       - the STORE wave: row f is complete once step f + 63 is written; it
-//         reads row f back from the ring (lane l: slot (f + l) mod R) and stores
-//         it as ONE row-contiguous 256*C-byte segment (buffer_store_dword{,x2,x4},
-//         1 KB at C = 4).  HBM sees only whole, aligned row segments.
-//     The two waves are coupled by two LDS counters (steps written / rows read);
-//     R = 64 + slack slots let the store wave lag by up to the slack.
-//   * The strip's right column (lane 63, column C-1) is shifted into a DPP
-//     wave_shl:1 register as it is computed and published per 64-row block as
-//     8-byte {tag, value} granules (agent-scope atomic stores; the data is the
-//     flag) for the strip to the right, which polls them -- the GPU analogue of
-//     idxarray-mt's per-row progress counters (idxarray-mt.cpp:8,44,50-56).
+//         s'(a, b) = s(a, b) - GAP comes from a per-lane 8-byte score table
+//         indexed by the (mapped) row character: ONE v_perm_b32 gives column
+//         k's scores for four consecutive steps.  up' is the lane's own
+//         register; left'/diag' of column k > 0 are the lane's own column k-1.
+//         Column 0 of the wave takes left' from lane l-1's column C-1 (DPP
+//         wave_shr:1, whose "old" operand feeds lane 0 from the FEED: a ring of
+//         the left neighbour's right column in LDS).  Each step's C results go
+//         to the wave's LDS ring indexed by ANTI-DIAGONAL (128 slots; slot =
+//         step mod 128) with one conflict-free ds_write_b(32*C) at a
+//         compile-time offset.  Compute waves issue no table stores: on gfx950
+//         a vector store holds its wave for ~45-190 cycles.  A lone wave
+//         issues one VALU per ~4 cycles, which is why a strip has several
+//         compute waves (one per SIMD) rather than wider lanes.
+//       - store waves (kSPR per compute wave): row f of ring j is complete once
+//         step f + 63 is written; they read rows back (lane l: slot (f + l)
+//         mod 128) and store each as ONE row-contiguous 256*C-byte segment
+//         (global_store_dwordx4).  HBM sees only whole, aligned row segments.
+//     The waves are coupled by LDS counters (steps written / rows read / feed
+//     rows published / iterations done).
+//   * Each compute wave reads its right column (lane 63, column C-1) back from
+//     its ring 16 rows at a time and publishes it: into the next compute
+//     wave's LDS feed ring (+ a counter), or -- for the strip's last wave -- as
+//     8-byte {tag, value} granules in HBM (agent-scope atomic stores; the data
+//     is the flag) for the next strip's first wave, which polls them -- the
+//     GPU analogue of idxarray-mt's per-row progress counters
+//     (idxarray-mt.cpp:8,44,50-56).
 //   * Strips are claimed from an atomic ticket in increasing order by a
 //     persistent grid, so a strip's producer is always already running:
 //     deadlock-free for any grid size / residency.
@@ -52,10 +65,29 @@ namespace nw {
 // s_memrealtime runs at 100 MHz on gfx9: 20 s watchdog for every bounded spin.
 constexpr uint64_t kTimeoutTicks = 100000000ull * 20ull;
 constexpr int32_t kDone = 0x7FFFFFFF;  // counter value: "no more waiting on me"
-constexpr int kStoreWaves = 2;         // store waves per strip workgroup
-#ifndef NW_BCAP
-#define NW_BCAP 0  // max older stores a store wave keeps in flight (0: no cap)
-#endif
+constexpr int32_t kDead = INT32_MIN;   // wait_counter: gave up (watchdog / error word)
+
+// Watchdog diagnosis: the first bounded wait that gives up records where
+// (ctrl[1] = error code, ctrl[2] = site << 24 | wave << 16 | LDS/granule word
+// offset, ctrl[3] = the value it needed, ctrl[4] = the value it last saw).
+__device__ __forceinline__ void give_up(uint32_t *ctrl, uint32_t code, uint32_t site,
+                                        const void *p, int64_t need, int64_t seen) {
+    if ((threadIdx.x & 63) != 0) return;
+    if (atomicCAS(ctrl + 1, 0u, code) == 0u) {
+        ctrl[2] = (site << 24) | ((threadIdx.x >> 6) << 16) | ((uint32_t)(uintptr_t)p & 0xFFFFu);
+        ctrl[3] = (uint32_t)need;
+        ctrl[4] = (uint32_t)seen;
+    }
+}
+
+// Compiler-only ordering of LDS accesses around the workgroup counters.  One
+// wave's LDS instructions execute in order, so a counter store placed after the
+// data it publishes (and a data load placed after the counter load that
+// allowed it) is ordered for the other waves; the barrier only stops the
+// compiler from moving plain loads/stores across the relaxed counter accesses.
+__device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
+constexpr int kR = 128;                // ring slots (anti-diagonals); 64 rows of slack
+constexpr int kFeedRows = 256;         // feed ring entries per compute wave
 
 template <int C> struct Vec;
 template <> struct Vec<1> { typedef int32_t T; };
@@ -80,23 +112,36 @@ __device__ __forceinline__ void set_comp(typename Vec<C>::T &v, int k, int32_t x
     }
 }
 
-// LDS of one workgroup: ring of R anti-diagonal slots (64*C int32 each), two
-// 64-row feed buffers, the counters.
-template <int C>
+// LDS of one workgroup: NC rings of kR anti-diagonal slots (64*C int32 each),
+// NC feed rings of kFeedRows int32, the counters.
+template <int C, int NC>
 struct Lay {
     static constexpr int kSlot = 4 * kWave * C;       // bytes per ring slot
-    // slots (64 + slack): two workgroups per CU at C = 4 and 2, four at C = 1
-    static constexpr int R = C == 4 ? 76 : C == 2 ? 152 : 148;
-    static constexpr int kRing = R * kSlot;          // ring bytes
-    static constexpr int kFeed = kRing;              // byte offset of the feed buffers
-    static constexpr int kCtl = kFeed + 2 * kWave * 4;
-    // counters: [0] steps written, [1 + b] rows read by store wave b, [3] strip
-    static constexpr int kBytes = kCtl + 16;
-    // compute wave: check ring space every kChk steps, publish progress every
-    // kPub steps (coarse only where the slack R - 64 allows it)
-    static constexpr int kChk = R - 64 >= 48 ? 16 : 4;
-    static constexpr int kPub = R - 64 >= 48 ? 8 : 4;
+    static constexpr int kRing = kR * kSlot;          // ring bytes (a power of two)
+    static constexpr int kFeed = NC * kRing;          // byte offset of the feed rings
+    static constexpr int kCtl = kFeed + NC * kFeedRows * 4;
+    // counters, 8 words per compute wave j: [0] steps written, [1] rows of its
+    // right column published into wave j+1's feed, [2] iterations done,
+    // [3 + q] rows read by its store wave q; then the strip word
+    static constexpr int kCtlWords = 8;
+    static constexpr int kStripWord = NC * kCtlWords;
+    static constexpr int kBytes = kCtl + (kStripWord + 4) * 4;
+    // store waves per compute wave, rows per store-wave batch (kSPR batches in
+    // flight <= 64 rows of ring slack)
+#ifdef NW_SPR
+    static constexpr int kSPR = NW_SPR;  // (tuning builds: make variant DEFS=-DNW_SPR=3)
+#else
+    static constexpr int kSPR = C == 4 ? 3 : 2;
+#endif
+    static constexpr int kBatch = C == 4 ? 8 : 16;
+    static constexpr int kWaves = NC * (1 + kSPR);
+    // compute wave: check ring space every kChk steps, publish progress every kPub
+    static constexpr int kChk = 16;
+    static constexpr int kPub = 8;
 };
+static_assert(Lay<4, 1>::kBytes <= 160 * 1024, "ring must fit a CU's LDS");
+static_assert(Lay<2, 2>::kBytes <= 160 * 1024, "ring must fit a CU's LDS");
+static_assert(Lay<1, 4>::kBytes <= 160 * 1024, "ring must fit a CU's LDS");
 
 __device__ __forceinline__ uint64_t gran_load(const uint64_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -121,8 +166,8 @@ __device__ __forceinline__ void ctr_store(int32_t *p, int32_t v) {
 // Bounded: gives up -- raising the error word -- after kTimeoutTicks, or at once
 // if another wave already raised it.  Returns the last value read; the caller
 // re-checks its tag.
-__device__ __noinline__ uint64_t wait_chunk(const uint64_t *g, uint32_t tag, int c,
-                                            uint32_t *ctrl) {
+__device__ __forceinline__ uint64_t wait_chunk(const uint64_t *g, uint32_t tag, int c,
+                                            uint32_t *ctrl, uint32_t site) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     const int lane = threadIdx.x & 63;
     const bool in_chunk = (lane >> 4) == c;
@@ -132,7 +177,7 @@ __device__ __noinline__ uint64_t wait_chunk(const uint64_t *g, uint32_t tag, int
         if (__all(!in_chunk || (uint32_t)(v >> 32) == tag)) return v;
         if (ctrl_load(ctrl + 1) != 0u) return v;
         if (__builtin_amdgcn_s_memrealtime() - t0 > kTimeoutTicks) {
-            if (lane == 0) atomicCAS(ctrl + 1, 0u, 1u);
+            give_up(ctrl, 1u, site, g, tag, (int64_t)(v >> 32));
             return v;
         }
     }
@@ -149,32 +194,35 @@ __device__ __forceinline__ int chunks_ready(uint64_t v, uint32_t tag) {
 }
 
 // Bounded spin until the LDS counter *p reaches `need`; returns the value seen
-// (kDone once the error word is raised or the watchdog expires).
-__device__ __noinline__ int32_t wait_counter(const int32_t *p, int32_t need, uint32_t *ctrl) {
+// (kDead once the error word is raised or the watchdog expires).
+__device__ __forceinline__ int32_t wait_counter(const int32_t *p, int32_t need, uint32_t *ctrl,
+                                             uint32_t site) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
         const int32_t v = __builtin_amdgcn_readfirstlane(ctr_load(p));
         if (v >= need) return v;
-        if (ctrl_load(ctrl + 1) != 0u) return kDone;
+        if (ctrl_load(ctrl + 1) != 0u) return kDead;
         if (__builtin_amdgcn_s_memrealtime() - t0 > kTimeoutTicks) {
-            if ((threadIdx.x & 63) == 0) atomicCAS(ctrl + 1, 0u, 3u);
-            return kDone;
+            give_up(ctrl, 3u, site, p, need, v);
+            return kDead;
         }
         __builtin_amdgcn_s_sleep(1);
     }
 }
 
-// Rows every store wave has read out of the ring (each publishes the start of
-// its next batch; all rows below the smallest are out).
-__device__ __forceinline__ int32_t rows_read(const int32_t *ctr) {
-    int32_t v = ctr_load(ctr + 1);
+// Rows every store wave of a ring has read out of it (each publishes the
+// start of its next batch; all rows below the smallest are out).
+template <int NS>
+__device__ __forceinline__ int32_t rows_read(const int32_t *rd) {
+    int32_t v = ctr_load(rd);
 #pragma unroll
-    for (int b = 1; b < kStoreWaves; ++b) v = min(v, ctr_load(ctr + 1 + b));
+    for (int q = 1; q < NS; ++q) v = min(v, ctr_load(rd + q));
     return v;
 }
-__device__ __forceinline__ void wait_rows_read(const int32_t *ctr, int32_t need, uint32_t *ctrl) {
+template <int NS>
+__device__ __forceinline__ void wait_rows_read(const int32_t *rd, int32_t need, uint32_t *ctrl) {
 #pragma unroll
-    for (int b = 0; b < kStoreWaves; ++b) (void)wait_counter(ctr + 1 + b, need, ctrl);
+    for (int q = 0; q < NS; ++q) (void)wait_counter(rd + q, need, ctrl, 1);
 }
 
 // Row characters of local iteration j (steps 64j .. 64j+63): lane l needs the
@@ -197,33 +245,38 @@ __device__ __forceinline__ void static_for(F &&f) {
 }
 
 // How a cell's substitution score is formed.
-//   SUB_PROF : query profile -- the row word holds s(a_k, b) - GAP per row as
-//              int8 (one profile per distinct column character, nw_profile);
-//              d = diag' + sext(byte):  ONE v_add_u32_sdwa, no compare
+//   SUB_PERM : the row words hold MAPPED row characters (index 0..7 of the
+//              character among s1's distinct ones, 7 = "in no column"); each
+//              lane keeps, per column k, the 8-byte table
+//              T_k[x] = s(a_k, char x) - GAP (int8).  v_perm_b32(T_k, word)
+//              yields column k's scores for the 4 rows of a row word (one
+//              byte per step), so per cell d = diag' + sext(byte): ONE
+//              v_add_u32_sdwa, no compare.  Needs <= 7 distinct column
+//              characters and both scores - GAP in int8.
 //   SUB_UNIT : match - mismatch == 1: d = diag' + mm' + [a == b]
-//              (v_cmp_eq_u32_sdwa -> vcc -> v_addc)
+//              (v_cmp_eq_u32_sdwa -> vcc -> v_addc) on raw characters
 //   SUB_GEN  : d = diag' + (a == b ? ms' : mm')  (v_cmp -> vcc -> v_cndmask, add)
 // The compare forms test raw byte equality, the reference's match test
-// (serial.cpp:23-24); ms' / mm' / the profile bytes have GAP pre-subtracted
-// because diag' = t + GAP.  On a lone gfx950 wave the vcc round trip costs
-// ~15 cycles per cell, which is why the profile form exists.
-enum Sub { SUB_PROF = 0, SUB_UNIT = 1, SUB_GEN = 2 };
+// (serial.cpp:23-24); ms' / mm' / the table bytes have GAP pre-subtracted
+// because diag' = t + GAP.
+enum Sub { SUB_PERM = 0, SUB_UNIT = 1, SUB_GEN = 2 };
 
 template <int QB, int KB, int MODE>
-__device__ __forceinline__ int32_t diag_plus_sub(uint32_t pk, uint32_t apk, int32_t diag,
+__device__ __forceinline__ int32_t diag_plus_sub(uint32_t w, uint32_t apk, int32_t diag,
                                                  int32_t msp, int32_t mmp) {
     int32_t d;
-    if constexpr (MODE == SUB_PROF) {
+    if constexpr (MODE == SUB_PERM) {
+        // w = v_perm result: byte QB = s'(a_k, row of step QB)
         asm("v_add_u32_sdwa %0, %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD "
             "src0_sel:DWORD src1_sel:BYTE_%c3"
             : "=v"(d)
-            : "v"(diag), "v"(pk), "i"(QB));
+            : "v"(diag), "v"(w), "i"(QB));
     } else if constexpr (MODE == SUB_UNIT) {
         asm volatile(
             "v_cmp_eq_u32_sdwa vcc, %1, %2 src0_sel:BYTE_%c4 src1_sel:BYTE_%c5\n\t"
             "v_addc_co_u32_e32 %0, vcc, %3, %6, vcc"
             : "=v"(d)
-            : "v"(pk), "v"(apk), "v"(diag), "i"(QB), "i"(KB), "v"(mmp)
+            : "v"(w), "v"(apk), "v"(diag), "i"(QB), "i"(KB), "v"(mmp)
             : "vcc");
     } else {
         int32_t sc;
@@ -231,98 +284,147 @@ __device__ __forceinline__ int32_t diag_plus_sub(uint32_t pk, uint32_t apk, int3
             "v_cmp_eq_u32_sdwa vcc, %1, %2 src0_sel:BYTE_%c5 src1_sel:BYTE_%c6\n\t"
             "v_cndmask_b32_e32 %0, %3, %4, vcc"
             : "=v"(sc)
-            : "v"(pk), "v"(apk), "v"(mmp), "v"(msp), "i"(QB), "i"(KB)
+            : "v"(w), "v"(apk), "v"(mmp), "v"(msp), "i"(QB), "i"(KB)
             : "vcc");
         d = diag + sc;
     }
     return d;
 }
 
-// Per-lane state of the compute wave on one strip.
+// Per-lane state of a compute wave on one strip.
 template <int C>
 struct Lanes {
-    int32_t u[C];     // t + GAP of the lane's current row, column k
-    int32_t dg;       // diag' of column 0 for the next step (= last step's left')
-    int32_t rr;       // RAMP: row of this lane at the current step
-    uint32_t apk;     // column characters of the lane, byte k = column k
-    int32_t outcol;   // shift register of the strip's right column
-    int32_t cb;       // last value read of the store wave's row counter
+    int32_t u[C];      // t + GAP of the lane's current row, column k
+    int32_t dg;        // diag' of column 0 for the next step (= last step's left')
+    int32_t rr;        // RAMP: row of this lane at the current step
+    uint32_t apk;      // raw column characters of the lane, byte k = column k
+    uint32_t tlo[C];   // SUB_PERM score tables: bytes 0..3 / 4..7 of T_k
+    uint32_t thi[C];
+    int32_t cb;        // last value read of the store waves' row counters
+    uint32_t rb[2];    // ring byte address of this lane's piece of slot 0 / 64
+    uint32_t rc[2];    // read-back address of the right column (see run_iter)
+    int32_t rcol;      // right-column value read back, published a few steps later
 };
 
-// The feed of one iteration: the left neighbour's right column for rows
-// 64*it .. 64*it+63, published there in 16-row chunks.  `ready` leading chunks
-// were found published when the iteration started; before the group that
-// first reads chunk c >= ready, run_iter waits for it (wait_chunk) and writes
-// its 16 feed values.
+// Where a compute wave's feed comes from.
+enum FeedSrc { FEED_BOUNDARY = 0, FEED_GRAN = 1, FEED_LDS = 2 };
+
+// The feed of one iteration: the left neighbour's right column (+ GAP) for rows
+// 64*it .. 64*it+63, in this wave's LDS feed ring.  `ready` leading 16-row
+// chunks were found there when the iteration started; before the group that
+// first reads chunk c >= ready, run_iter waits for it: FEED_GRAN polls the
+// granules (wait_chunk) and writes the 16 values itself, FEED_LDS waits for the
+// left compute wave's published-rows counter.
 struct Feed {
-    const uint64_t *g;  // this lane's granule of the block (left neighbour's slot)
+    int src;             // FeedSrc (uniform)
+    const uint64_t *g;   // FEED_GRAN: this lane's granule of the block
+    const int32_t *pub;  // FEED_LDS: the left wave's published-rows counter
+    int32_t *ring;       // this wave's feed ring (kFeedRows int32)
     uint32_t tag;
     int ready;
     int32_t gap;
     uint32_t nslow;
     uint64_t wticks;
+    uint64_t rticks;     // debug trace: time spent waiting for ring space
     bool dead;
-    bool trace_pub;     // debug trace: stamp the publish of chunk 0 in this iteration
+    bool trace_pub;      // debug trace: stamp the publish of chunk 0 in this iteration
     uint64_t tpub;
 };
 
-// Row words per lane and iteration: one per column of the lane in the profile
-// form (each column has its own character's profile), one in the compare forms.
-template <int C, int MODE>
-constexpr int npk() { return MODE == SUB_PROF ? C : 1; }
+// Where a compute wave's right column goes.
+struct Out {
+    bool lds;            // into the next compute wave's feed ring (else granules)
+    int32_t *ring;       // next wave's feed ring
+    int32_t *pub;        // my published-rows counter
+    int32_t gap;
+};
 
 // 64 wavefront steps of local iteration `it` (steps s = 64*it + u, u < 64) of
-// the compute wave.  Step s: compute row s - l on every lane l, write the
-// results to ring slot s mod R, shift the strip's right column (lane 63's
-// column C-1, row s - 63) into outcol.  Every kPub steps the steps-written
-// counter is published; every kChk steps the slots the next kChk overwrite are
-// checked free (rows read by the store wave; the counter value was read kChk
-// steps earlier, so its LDS latency is hidden).
-//   pk   : row words of this iteration (load_packs), [npk][4] x 16 rows each
-//   sb   : slot of step 64*it (= 64*it mod R)
-//   gp   : this lane's granule of block it-1 (the right column is published in
-//          16-row chunks, after steps 14, 30, 46, 62)
-//   F    : the feed of this iteration (chunks not yet published are waited for)
-template <int C, int MODE, bool RAMP>
-__device__ __forceinline__ void run_iter(char *__restrict__ lds, int it,
-                                         const u32x4 (&pk)[npk<C, MODE>()][4], int32_t msp,
-                                         int32_t mmp, int32_t gap, Lanes<C> &S, int sb,
-                                         uint64_t *gp, uint64_t tagw, uint32_t *ctrl, Feed &F,
+// a compute wave.  Step s: compute row s - l on every lane l, write the
+// results to ring slot s mod 128 (= 64*HALF + u: a compile-time offset from
+// S.rb[HALF]).  Every kPub steps the steps-written counter is published; every
+// kChk steps the slots the next kChk overwrite are checked free (rows read by
+// the store waves; the counter value was read kChk steps earlier, so its LDS
+// latency is hidden).
+//   pk   : row words of this iteration (load_packs), 4 x 16 rows
+//   b    : block whose right column this iteration publishes (it - 1): rows
+//          64b + 16c + i, written by lane 63 at steps 64it + 16c + i - 1, are
+//          read back from the ring by lanes i < 16 after step 16c + 14 and
+//          published three steps later (chunk 3: after the last step)
+//   gp   : this lane's granule of block b (granule output)
+//   F    : the feed of this iteration (chunks not yet there are waited for)
+template <int C, int NC, int MODE, bool RAMP, int HALF>
+__device__ __forceinline__ void run_iter(char *__restrict__ lds, int it, const u32x4 (&pk)[4],
+                                         int32_t msp, int32_t mmp, int32_t gap, Lanes<C> &S,
+                                         int32_t *ctr, const int32_t *rd, int b, uint64_t *gp,
+                                         uint64_t tagw, const Out &O, uint32_t *ctrl, Feed &F,
                                          int lane) {
     typedef typename Vec<C>::T VT;
-    typedef Lay<C> L;
-    int32_t *ctr = (int32_t *)(lds + L::kCtl);
-    const int4 *feed4 = (const int4 *)(lds + L::kFeed + ((it & 1) << 8));
+    typedef Lay<C, NC> L;
+    const int4 *feed4 = (const int4 *)(F.ring + ((it & 3) << 6));
     int4 fq = feed4[0];
     const int s0 = it * 64;
+    // Ring base of this half.  The barrier keeps LICM from hoisting 64 per-step
+    // addresses out of the strip loop (they would stay live in registers); the
+    // mask proves the base non-negative, so each step's 64*HALF+u slot offset
+    // folds into the ds_write offset field.
+    uint32_t rbase = S.rb[HALF];
+    asm volatile("" : "+v"(rbase));
+    rbase &= 0x3FFFFu;
+    char *ringw = lds + rbase;
+    // publish chunk c of block b (lanes i < 16 hold rows 64b + 16c + i)
+    auto publish = [&](int c) {
+        if (b < 0) return;
+        if (O.lds) {
+            if (lane < 16) O.ring[(64 * b + 16 * c + lane) & (kFeedRows - 1)] = S.rcol + O.gap;
+            lds_order();
+            ctr_store(O.pub, 64 * b + 16 * c + 16);
+        } else if (lane < 16) {
+            gran_store(gp + 16 * c, tagw | (uint32_t)S.rcol);
+        }
+    };
     static_for<0, 16>([&](auto gc) {
         constexpr int g = decltype(gc)::value;
         // ring space for steps s0+4g .. s0+4g+kChk-1: their slots held
-        // anti-diagonals s - R, last needed by row s - R, so rows
-        // <= s0 + 4g + kChk - 1 - R must have been read
+        // anti-diagonals s - kR, last needed by row s - kR, so rows
+        // <= s0 + 4g + kChk - 1 - kR must have been read
         if constexpr ((4 * g) % L::kChk == 0) {
-            const int32_t need = s0 + 4 * g + L::kChk - L::R;
-            if (__builtin_amdgcn_readfirstlane(S.cb) < need) wait_rows_read(ctr, need, ctrl);
-            S.cb = rows_read(ctr);  // for the next check (kChk steps on)
+            const int32_t need = s0 + 4 * g + L::kChk - kR;
+            if (__builtin_amdgcn_readfirstlane(S.cb) < need) {
+                const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
+                wait_rows_read<L::kSPR>(rd, need, ctrl);
+                F.rticks += __builtin_amdgcn_s_memrealtime() - w0;  // (trace: ring back-pressure)
+            }
+            S.cb = rows_read<L::kSPR>(rd);  // for the next check (kChk steps on)
+            lds_order();                    // ring writes after the check
         }
         // chunk (g+1)/4 is read by the feed load below: wait for it if it was
-        // not yet published when the iteration started
+        // not there when the iteration started
         if constexpr ((g & 3) == 3 && g + 1 < 16) {
             constexpr int c = (g + 1) >> 2;
             if (F.ready <= c) {
                 const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
-                const uint64_t v = wait_chunk(F.g, F.tag, c, ctrl);
-                F.dead |= !__all((lane >> 4) != c || (uint32_t)(v >> 32) == F.tag);
+                if (F.src == FEED_GRAN) {
+                    const uint64_t v = wait_chunk(F.g, F.tag, c, ctrl, 2);
+                    F.dead |= !__all((lane >> 4) != c || (uint32_t)(v >> 32) == F.tag);
+                    if ((lane >> 4) == c) F.ring[((it & 3) << 6) + lane] = (int32_t)(uint32_t)v + F.gap;
+                } else {
+                    F.dead |= wait_counter(F.pub, s0 + 16 * (c + 1), ctrl, 3) == kDead;
+                    lds_order();  // feed reads after the counter that published them
+                }
                 F.nslow += 1;
                 F.wticks += __builtin_amdgcn_s_memrealtime() - w0;
-                if ((lane >> 4) == c)
-                    ((int32_t *)(lds + L::kFeed))[((it & 1) << 6) + lane] =
-                        (int32_t)(uint32_t)v + F.gap;
                 F.ready = c + 1;
             }
         }
         const int4 fcur = fq;
         if constexpr (g + 1 < 16) fq = feed4[g + 1];
+        const uint32_t word = pk[g >> 2][g & 3];  // row characters of steps 4g .. 4g+3
+        uint32_t sc[C];
+        if constexpr (MODE == SUB_PERM) {
+#pragma unroll
+            for (int k = 0; k < C; ++k) sc[k] = __builtin_amdgcn_perm(S.thi[k], S.tlo[k], word);
+        }
         static_for<0, 4>([&](auto qc) {
             constexpr int q = decltype(qc)::value;
             constexpr int u = 4 * g + q;
@@ -340,8 +442,8 @@ __device__ __forceinline__ void run_iter(char *__restrict__ lds, int it,
             VT tv;
             static_for<0, C>([&](auto kc) {
                 constexpr int k = decltype(kc)::value;
-                const uint32_t pkw = pk[MODE == SUB_PROF ? k : 0][g >> 2][g & 3];
-                const int32_t d = diag_plus_sub<q, k, MODE>(pkw, S.apk, diag, msp, mmp);
+                const uint32_t w = MODE == SUB_PERM ? sc[k] : word;
+                const int32_t d = diag_plus_sub<q, k, MODE>(w, S.apk, diag, msp, mmp);
                 int32_t t = max(max(d, S.u[k]), left);  // max(diag+s, up+GAP, left+GAP)
                 diag = S.u[k];
                 if constexpr (RAMP) {
@@ -355,39 +457,49 @@ __device__ __forceinline__ void run_iter(char *__restrict__ lds, int it,
                 left = S.u[k];
                 set_comp<C>(tv, k, t);
             });
-            // ring slot (s0 + u) mod R; sb + u < R + 64 wraps at most once
-            const int slot = sb + u >= L::R ? sb + u - L::R : sb + u;
-            *(VT *)(lds + slot * L::kSlot + lane * (4 * C)) = tv;
-            S.outcol = __builtin_amdgcn_update_dpp(comp<C>(tv, C - 1), S.outcol,
-                                                   0x130 /*wave_shl:1*/, 0xF, 0xF, false);
-            // after step 14 + 16c outcol's lanes 48..63 hold rows 64(it-1) + 16c + 0..15
-            // of the right column: publish that chunk (lane l -> row 64(it-1) + l - 48 + 16c)
+            *(VT *)(ringw + u * L::kSlot) = tv;  // ring slot 64*HALF + u
+            // right column of block b, chunk c = u / 16: read back after the
+            // step that completed it, publish three steps later
             if constexpr ((u & 15) == 14) {
-                if (lane >= 48) gran_store(gp + (16 * (u >> 4) - 48), tagw | (uint32_t)S.outcol);
-                if constexpr (u == 14) {
+                constexpr int c = u >> 4;
+                // lane i < 16: slot (64*HALF + 16c + i - 1) mod kR, lane 63's last column
+                const uint32_t a = (HALF == 0 && c == 0) ? S.rc[0] : S.rc[1] + (64 * HALF + 16 * c) * L::kSlot;
+                S.rcol = *(const int32_t *)(lds + a);
+            }
+            if constexpr ((u & 15) == 1 && u > 16) {
+                publish((u >> 4) - 1);
+                if constexpr (u == 17) {
                     if (F.trace_pub) F.tpub = __builtin_amdgcn_s_memrealtime();
                 }
             }
-            if constexpr ((u + 1) % L::kPub == 0) ctr_store(ctr, s0 + u + 1);  // steps written
+            if constexpr ((u + 1) % L::kPub == 0) {
+                lds_order();
+                ctr_store(ctr, s0 + u + 1);  // steps written
+            }
         });
     });
+    publish(3);
 }
 
-// The compute wave on strip p.
-template <int C, int MODE>
-__device__ void compute_strip(const FillArgs &A, char *__restrict__ lds, int p, int lane) {
-    typedef Lay<C> L;
-    constexpr int NPK = npk<C, MODE>();
+// Compute wave j of strip p.
+template <int C, int NC, int MODE>
+__device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restrict__ lds, int p,
+                                              int j, int lane) {
+    typedef Lay<C, NC> L;
     const int32_t gap = A.gap;
     const int32_t msp = A.match - gap, mmp = A.mismatch - gap;
-    const int64_t c0 = (int64_t)p * (64 * C);
+    const int64_t c0 = A.col0 + (int64_t)p * (NC * 64 * C) + (int64_t)j * (64 * C);
     const int64_t cl = c0 + (int64_t)C * lane;  // first column of this lane
-    int32_t *ctr = (int32_t *)(lds + L::kCtl);
+    int32_t *ctr = (int32_t *)(lds + L::kCtl) + j * L::kCtlWords;
+    const int32_t *rd = ctr + 3;  // rows read by my store waves
     bool dead = false;
     // Row 0: the boundary t[0][c] = c*GAP (serial.cpp:16), or -- for a row band
     // (mpi-horz.cpp:16-40) -- the previous band's last row, taken from its halo
-    // granules once they carry this launch's tag (bounded wait).
+    // granules once they carry this launch's tag (bounded wait).  bnd0 = t[0][0]
+    // (column 0 of the halo for a band), needed when col0 = 1 puts column 0
+    // outside the strips.
     int32_t top[C];
+    int32_t bnd0 = 0;
 #pragma unroll
     for (int k = 0; k < C; ++k) top[k] = (int32_t)((cl + k) * (int64_t)gap);
     if (A.halo_in != nullptr) {
@@ -402,120 +514,172 @@ __device__ void compute_strip(const FillArgs &A, char *__restrict__ lds, int p, 
                 top[k] = (int32_t)(uint32_t)g;
                 ok &= (uint32_t)(g >> 32) == A.halo_tag;
             }
+            const uint64_t g0 = __hip_atomic_load(A.halo_in, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            bnd0 = (int32_t)(uint32_t)g0;
+            ok &= (uint32_t)(g0 >> 32) == A.halo_tag;
             if (__all(ok)) break;
             if (ctrl_load(A.ctrl + 1) != 0u) { dead = true; break; }
             if (__builtin_amdgcn_s_memrealtime() - h0 > kTimeoutTicks) {
-                if (lane == 0) atomicCAS(A.ctrl + 1, 0u, 2u);
+                give_up(A.ctrl, 2u, 4, A.halo_in, A.halo_tag, 0);
                 dead = true;
                 break;
             }
             __builtin_amdgcn_s_sleep(4);
         }
     }
+    // t[0][0] for the store waves (boundary column 0 when col0 = 1); they read it
+    // only after this wave's first steps-written counter
+    if (j == 0) ((int32_t *)(lds + L::kCtl))[L::kStripWord + 1] = bnd0;
     Lanes<C> S;
     S.apk = 0;
+    // SUB_PERM tables: T_k[x] = s(a_k, chars[x]) - GAP for x < 8 (x = 7 and any
+    // x >= nprof: a row character in no column, always a mismatch)
+    const uint32_t mmb = ((uint32_t)mmp & 255u) * 0x01010101u;
 #pragma unroll
     for (int k = 0; k < C; ++k) {
         const int64_t c = cl + k;
         const uint32_t a = (c >= 1 && c <= A.n1) ? (uint32_t)A.s1[c - 1] : 0u;
         S.apk |= a << (8 * k);
         S.u[k] = top[k] + gap;  // t[0][c] + GAP
+        if constexpr (MODE == SUB_PERM) {
+            const uint32_t x = (c >= 1 && c <= A.n1) ? (uint32_t)A.charmap[a] : 0xFFu;
+            const uint32_t msb = (uint32_t)msp & 255u;
+            const uint32_t sh = 8u * (x & 3u), keep = ~(255u << sh), put = msb << sh;
+            S.tlo[k] = x < 4u ? ((mmb & keep) | put) : mmb;
+            S.thi[k] = (x >= 4u && x < 8u) ? ((mmb & keep) | put) : mmb;
+        } else {
+            S.tlo[k] = S.thi[k] = 0u;
+        }
     }
     S.dg = 0;
     S.rr = -lane - 1;
-    S.outcol = 0;
     S.cb = 0;
+    S.rcol = 0;
+    S.rb[0] = (uint32_t)(j * L::kRing) + (uint32_t)lane * (4u * C);
+    S.rb[1] = S.rb[0] + 64u * L::kSlot;
+    // right-column read-back: lane i < 16 reads slot (64*HALF + 16c + i - 1) mod kR
+    // at lane 63's last column (byte kSlot - 4 of the slot).  rc[1] + offset
+    // covers every (HALF, c) but (0, 0), whose lane 0 wraps to slot kR - 1: rc[0].
+    {
+        const int i = lane & 15;
+        S.rc[1] = (uint32_t)(j * L::kRing + i * L::kSlot - 4);  // (i - 1) * kSlot + kSlot - 4
+        S.rc[0] = i == 0 ? (uint32_t)(j * L::kRing + L::kRing - 4) : S.rc[1];
+    }
 
-    const bool has_left = p > 0;
+    // Feed: the strip's first wave takes the previous strip's right column from
+    // its granules (or, for strip 0, the boundary column); later waves take
+    // wave j-1's from LDS.  Output: the strip's last wave publishes granules,
+    // the others feed wave j+1.
+    Feed F;
+    F.src = j > 0 ? FEED_LDS : p > 0 ? FEED_GRAN : FEED_BOUNDARY;
+    F.ring = (int32_t *)(lds + L::kFeed) + j * kFeedRows;
+    F.pub = (const int32_t *)(lds + L::kCtl) + (j > 0 ? j - 1 : 0) * L::kCtlWords + 1;
+    F.tag = A.tagbase + (uint32_t)p;
+    F.gap = gap;
+    F.nslow = 0;
+    F.wticks = 0;
+    F.rticks = 0;
+    F.dead = dead;  // (a halo wait may already have given up)
+    F.trace_pub = false;
+    F.tpub = 0;
+    Out O;
+    O.lds = j + 1 < NC;
+    O.ring = (int32_t *)(lds + L::kFeed) + (j + 1 < NC ? j + 1 : j) * kFeedRows;
+    O.pub = ctr + 1;
+    O.gap = gap;
+    const int32_t *next_done = ctr + L::kCtlWords + 2;  // iterations done by wave j+1
+
     const uint64_t *gin = A.gran + (int64_t)((p + A.M - 1) % A.M) * A.gstride + lane;
     uint64_t *gout = A.gran + (int64_t)(p % A.M) * A.gstride;
-    const uint32_t tag_in = A.tagbase + (uint32_t)p;
     const uint64_t tagw = (uint64_t)(A.tagbase + (uint32_t)p + 1u) << 32;
     const int nblocks = A.nblocks;
     const int lastb = nblocks - 1;
     uint64_t *gscr = (uint64_t *)(A.scratch + (int64_t)blockIdx.x * kScratchWords) + lane;
 
-    // Row words: the raw s2 bytes (compare forms), or per column k the profile
-    // of the lane's character a_k (profile form; nw_profile).
-    const u32x4 *pkp[NPK];
-    if constexpr (MODE == SUB_PROF) {
-#pragma unroll
-        for (int k = 0; k < C; ++k) {
-            const uint32_t m = min((uint32_t)A.charmap[(S.apk >> (8 * k)) & 255u], kMaxProf - 1u);
-            pkp[k] = (const u32x4 *)A.prof + (int64_t)m * A.prof_stride;
-        }
-    } else {
-        pkp[0] = (const u32x4 *)A.rowpack;
-    }
+    const u32x4 *pkp = (const u32x4 *)A.rowpack;
     // Prefetch pipeline: the left neighbour's granules (feed) and the row words
-    // are loaded PD iterations ahead into (PD+1)-deep register rings, so no wait
-    // for a load falls inside the steps (PD = 2; 1 when four profile words per
-    // iteration would not fit in registers).  Buffer = iteration mod NB; all
-    // loads unconditional (clamped indices).
-    constexpr int NB = NPK >= 4 ? 2 : 3, PD = NB - 1;
+    // are loaded PD iterations ahead into NB-deep register rings, so no wait for
+    // a load falls inside the steps.  Buffer = iteration mod NB; all loads
+    // unconditional (clamped indices).  NB is even so that the ring half
+    // (iteration parity) is a function of the buffer index.
+    constexpr int NB = 4, PD = NB - 1;
     uint64_t gb[NB];
-    u32x4 pkb[NB][NPK][4];
+    u32x4 pkb[NB][4];
 #pragma unroll
     for (int i = 0; i < PD; ++i) {
         gb[i] = gran_load(gin + (int64_t)min(i, lastb) * 64);  // block i, for iteration i
-#pragma unroll
-        for (int k = 0; k < NPK; ++k) load_packs(pkp[k], i, lane, pkb[i][k]);
+        load_packs(pkp, i, lane, pkb[i]);
     }
 
-    Feed F;
-    F.tag = tag_in;
-    F.gap = gap;
-    F.nslow = 0;
-    F.wticks = 0;
-    F.dead = dead;  // (a halo wait may already have given up)
     const uint64_t tstart = __builtin_amdgcn_s_memrealtime();
     const uint64_t cstart = __builtin_amdgcn_s_memtime();
     uint64_t tq1 = 0, tmid = 0;  // trace: times iterations nblocks/4 and nblocks/2 started
-    uint64_t tpub = 0, tsee = 0, twait = 0;  // trace: publish / see / wait start, block nblocks/2 chunk 0
-    F.trace_pub = false;
-    F.tpub = 0;
+    uint64_t tsee = 0, twait = 0;  // trace: see / wait start, block nblocks/2 chunk 0
 
-    // Iteration it: feed for block it (consumes buffer it % 3), prefetch for it+2
-    // (into buffer (it+2) % 3), 64 steps, block it-1's right column published.
-    // A watchdog trip marks the strip dead; it is abandoned at the boundary.
+    // Iteration it: feed for block it (consumes buffer it % NB), prefetch for
+    // it+PD, 64 steps, block it-1's right column published.  A watchdog trip
+    // marks the strip dead; it is abandoned at the boundary.
     auto iter = [&](int it, auto cons_c, auto ramp_c) {
         constexpr int CONS = decltype(cons_c)::value;  // it % NB
         constexpr int ISS = (CONS + PD) % NB;          // (it + PD) % NB
+        constexpr int HALF = CONS & 1;                 // it % 2
         constexpr bool RAMP = decltype(ramp_c)::value;
+        const bool traced = A.trace != nullptr && it == nblocks / 2;
         if (A.trace != nullptr) {
             if (it == nblocks / 4) tq1 = __builtin_amdgcn_s_memrealtime();
-            if (it == nblocks / 2) tmid = __builtin_amdgcn_s_memrealtime();
+            if (traced) tmid = __builtin_amdgcn_s_memrealtime();
             F.trace_pub = it == nblocks / 2 + 1;
         }
-        {
-            int32_t fvv = kNeg;
-            F.ready = 4;
-            if (has_left && it < nblocks) {
+        // feed-ring space for this iteration's publish (rows of block it-1 land
+        // where rows of block it-5 were): wave j+1 must have finished it-5
+        if (O.lds && it >= 5) F.dead |= wait_counter(next_done, it - 4, A.ctrl, 5) == kDead;
+        F.ready = 4;
+        if (it < nblocks) {
+            if (F.src == FEED_GRAN) {
                 uint64_t gv = gb[CONS];  // block it, loaded PD iterations ago
                 F.g = gin + (int64_t)it * 64;
-                F.ready = chunks_ready(gv, tag_in);
+                F.ready = chunks_ready(gv, F.tag);
                 if (F.ready == 0) {  // chunk 0 is needed right away
                     const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
-                    if (A.trace != nullptr && it == nblocks / 2) twait = w0;
-                    gv = wait_chunk(F.g, tag_in, 0, A.ctrl);
-                    F.dead |= !__all((lane >> 4) != 0 || (uint32_t)(gv >> 32) == tag_in);
+                    if (traced) twait = w0;
+                    gv = wait_chunk(F.g, F.tag, 0, A.ctrl, 6);
+                    F.dead |= !__all((lane >> 4) != 0 || (uint32_t)(gv >> 32) == F.tag);
                     F.nslow += 1;
                     F.wticks += __builtin_amdgcn_s_memrealtime() - w0;
-                    F.ready = max(1, chunks_ready(gv, tag_in));
+                    F.ready = max(1, chunks_ready(gv, F.tag));
                 }
-                fvv = (int32_t)(uint32_t)gv + gap;
-                if (A.trace != nullptr && it == nblocks / 2) tsee = __builtin_amdgcn_s_memrealtime();
+                F.ring[((it & 3) << 6) + lane] = (int32_t)(uint32_t)gv + gap;
+            } else if (F.src == FEED_LDS) {
+                int32_t pv = __builtin_amdgcn_readfirstlane(ctr_load(F.pub));
+                if (pv < it * 64 + 16) {
+                    const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
+                    if (traced) twait = w0;
+                    pv = wait_counter(F.pub, it * 64 + 16, A.ctrl, 7);
+                    F.dead |= pv == kDead;
+                    F.nslow += 1;
+                    F.wticks += __builtin_amdgcn_s_memrealtime() - w0;
+                }
+                F.ready = min(4, (pv - it * 64) >> 4);
+                lds_order();  // feed reads after the counter that published them
+            } else {
+                // strip 0, wave 0: left of column col0 is the boundary column:
+                // t[r][0] + GAP with col0 = 1, "minus infinity" when col0 = 0 (the
+                // lane holding column 0 then computes t[r][0] = t[r-1][0] + GAP)
+                const int32_t r = it * 64 + lane;
+                F.ring[((it & 3) << 6) + lane] = A.col0 ? bnd0 + (r + 1) * gap : kNeg;
             }
-            ((int32_t *)(lds + L::kFeed))[((it & 1) << 6) + lane] = fvv;
+            if (traced) tsee = __builtin_amdgcn_s_memrealtime();
+        } else if (F.src != FEED_LDS) {
+            // past the last block: every lane's row is beyond n2
+            F.ring[((it & 3) << 6) + lane] = kNeg;
         }
         gb[ISS] = gran_load(gin + (int64_t)min(it + PD, lastb) * 64);
-#pragma unroll
-        for (int k = 0; k < NPK; ++k) load_packs(pkp[k], it + PD, lane, pkb[ISS][k]);
+        load_packs(pkp, it + PD, lane, pkb[ISS]);
         const int b = it - 1;  // block whose right column this iteration publishes
         uint64_t *gp = (b >= 0 && b < nblocks) ? gout + (int64_t)b * 64 + lane : gscr;
-        const int sb = __builtin_amdgcn_readfirstlane((int)(((uint32_t)it * 64u) % (uint32_t)L::R));
-        run_iter<C, MODE, RAMP>(lds, it, pkb[CONS], msp, mmp, gap, S, sb, gp, tagw, A.ctrl, F,
-                                lane);
+        run_iter<C, NC, MODE, RAMP, HALF>(lds, it, pkb[CONS], msp, mmp, gap, S, ctr, rd, b, gp, tagw,
+                                          O, A.ctrl, F, lane);
+        ctr_store(ctr + 2, it + 1);  // iterations done (feed-ring space for wave j-1)
         dead = F.dead;
     };
     // iteration 0 ramps the wavefront in (lanes above row 1 hold row 0); row
@@ -523,99 +687,115 @@ __device__ void compute_strip(const FillArgs &A, char *__restrict__ lds, int p, 
     const int nit = nblocks + 1;
     iter(0, std::integral_constant<int, 0>{}, std::true_type{});
     for (int it = 1; it < nit && !dead; it += NB) {
-        iter(it, std::integral_constant<int, 1 % NB>{}, std::false_type{});
+        iter(it, std::integral_constant<int, 1>{}, std::false_type{});
         if (it + 1 >= nit || dead) break;
-        iter(it + 1, std::integral_constant<int, 2 % NB>{}, std::false_type{});
-        if constexpr (NB == 3) {
-            if (it + 2 >= nit || dead) break;
-            iter(it + 2, std::integral_constant<int, 0>{}, std::false_type{});
-        }
+        iter(it + 1, std::integral_constant<int, 2>{}, std::false_type{});
+        if (it + 2 >= nit || dead) break;
+        iter(it + 2, std::integral_constant<int, 3>{}, std::false_type{});
+        if (it + 3 >= nit || dead) break;
+        iter(it + 3, std::integral_constant<int, 0>{}, std::false_type{});
     }
-    // every row is in the ring (or the strip is abandoned): release the store wave
+    // every row is in the ring (or the strip is abandoned): release the store
+    // waves and the compute waves waiting on me
     ctr_store(ctr, kDone);
+    ctr_store(ctr + 1, kDone);
+    ctr_store(ctr + 2, kDone);
     if (A.trace != nullptr && lane == 0) {
         uint64_t *tr = A.trace + (int64_t)p * kTraceWords;
-        tr[0] = tstart;
-        tr[1] = __builtin_amdgcn_s_memrealtime();
-        tr[2] = F.nslow;
-        tr[3] = F.wticks;
-        tr[4] = tq1;
-        tr[5] = tmid;
-        tr[6] = cstart;                          // shader clock (s_memtime)
-        tr[7] = __builtin_amdgcn_s_memtime();
-        tr[8] = F.tpub;
-        tr[9] = tsee;
-        tr[10] = twait;
+        if (j == 0) {
+            tr[0] = tstart;
+            tr[2] = F.nslow;
+            tr[3] = F.wticks;
+            tr[4] = tq1;
+            tr[5] = tmid;
+            tr[6] = cstart;  // shader clock (s_memtime)
+            tr[9] = tsee;
+            tr[10] = twait;
+            tr[11] = F.rticks;
+        }
+        if (j == NC - 1) {
+            tr[1] = __builtin_amdgcn_s_memrealtime();
+            tr[7] = __builtin_amdgcn_s_memtime();
+            tr[8] = F.tpub;
+            tr[12] = F.rticks;
+            tr[13] = F.wticks;
+        }
     }
 }
 
-// The store wave on strip p: rows 0 .. n2 leave the ring as whole row segments.
-// One 16-byte-per-lane store covers NR = 4/C rows (1 KB: a row of a C = 4 strip,
-// two rows of a C = 2 strip): B-lane l takes row f + l / (16C), columns
-// 4 * (l % (16C)) .. +3, i.e. the pieces of the NR compute lanes
-// a = NR * (l % (16C)) + m that wrote them, each in slot (row + a) mod R.
-// Rows go in batches of BATCH, dealt round robin to the kStoreWaves store waves
-// (b = this wave): wait until the compute wave has written the batch, read it
-// from the ring, store it, then release its slots.  Under full HBM load one
-// store instruction holds its wave for ~190 cycles, which is why one compute
-// wave has several store waves.
-template <int C>
-__device__ void store_strip(const FillArgs &A, char *__restrict__ lds, int p, int lane, int b) {
+// Store wave q of compute wave j on strip p: rows 0 .. n2 of ring j leave as
+// whole row segments.  One 16-byte-per-lane store covers NR = 4/C rows (1 KB:
+// a row of a C = 4 ring, two rows of a C = 2 ring): lane l takes row
+// f + l / (16C), columns 4 * (l % (16C)) .. +3, i.e. the pieces of the NR
+// compute lanes a = NR * (l % (16C)) + m that wrote them, each in slot
+// (row + a) mod kR.  Rows go in batches of kBatch, dealt round robin to the
+// kSPR store waves of the ring: wait until the compute wave has written the
+// batch, read it from the ring, store it, then release its slots.  Under full
+// HBM load one store instruction holds its wave for ~190 cycles, which is why
+// one compute wave has several store waves.
+template <int C, int NC>
+__device__ __forceinline__ void store_strip(const FillArgs &A, char *__restrict__ lds, int p,
+                                            int j, int q, int lane) {
     typedef typename Vec<C>::T VT;
-    typedef Lay<C> L;
+    typedef Lay<C, NC> L;
     constexpr int NR = 4 / C;                  // rows per store instruction
     constexpr int Q = 16 * C;                  // lanes per row
-    constexpr int BATCH = C == 4 ? 4 : 16;     // rows per batch (ring slack: R - 64)
+    constexpr int BATCH = L::kBatch;
+    constexpr int NS = L::kSPR;
     constexpr int NG = BATCH / NR;             // stores per batch
-    constexpr uint32_t kRingB = (uint32_t)L::kRing;
-    int32_t *ctr = (int32_t *)(lds + L::kCtl);
-    const int64_t c0 = (int64_t)p * (64 * C);
+    constexpr uint32_t kMask = (uint32_t)L::kRing - 1u;
+    int32_t *ctr = (int32_t *)(lds + L::kCtl) + j * L::kCtlWords;
+    const char *ring = lds + j * L::kRing;
+    const int64_t c0 = A.col0 + (int64_t)p * (NC * 64 * C) + (int64_t)j * (64 * C);
     const int32_t nrows = (int32_t)(A.n2 + 1);
     const bool timing = (A.flags & 1) != 0;
     const int ro = lane / Q, cq = lane % Q;
-    const bool col_ok = c0 + 4 * cq < A.pitch;  // the last strip may overhang the pitch
+    // the last strip may overhang the pitch: store only 16-byte pieces that lie
+    // wholly inside the row (with col0 = 1 a piece straddling the pitch would
+    // reach the next row's column 0; nw_table_pitch leaves room for column n1)
+    const bool col_ok = c0 + 4 * cq + 4 <= A.pitch;
     const int64_t rowb = timing ? 0 : A.pitch * 4;
     char *scr = (char *)(A.scratch + (int64_t)blockIdx.x * kScratchWords);
-    const int32_t f0 = b * BATCH;
+    const int32_t f0 = q * BATCH;
     char *rowp = timing ? scr : (char *)(A.table + c0) + (int64_t)f0 * rowb;
     const uint32_t voff = (uint32_t)(ro * rowb) + (uint32_t)cq * 16u;
+    // col0 = 1: strip 0's first ring also stores the boundary column 0,
+    // t[r][0] = t[0][0] + r*GAP (t[0][0] = 0, or the halo's column 0 for a band)
+    const bool bcol = A.col0 != 0 && p == 0 && j == 0 && !timing;
+    int32_t bnd0 = 0;  // t[0][0]: from compute wave 0 (after its halo wait), read below
+    const int32_t *bnd0p = (const int32_t *)(lds + L::kCtl) + L::kStripWord + 1;
     uint32_t pa[NR];  // ring byte address of piece m of this lane's row
 #pragma unroll
     for (int m = 0; m < NR; ++m) {
         const int a = NR * cq + m;
-        pa[m] = (uint32_t)((f0 + ro + a) % L::R) * L::kSlot + (uint32_t)a * (4u * C);
+        pa[m] = (uint32_t)((f0 + ro + a) % kR) * L::kSlot + (uint32_t)a * (4u * C);
     }
-    auto adv = [&](uint32_t x, uint32_t rows) {  // `rows` (< R) rows further down the ring
-        x += rows * L::kSlot;
-        return x >= kRingB ? x - kRingB : x;
-    };
-    int32_t *mine = ctr + 1 + b;
+    // `rows` further down the ring (the piece offset a * 4C < kSlot survives the mask)
+    auto adv = [&](uint32_t x, uint32_t rows) { return (x + rows * L::kSlot) & kMask; };
+    int32_t *mine = ctr + 3 + q;
     int32_t avail = 0;  // rows complete in the ring (steps written - 63)
-    for (int32_t f = f0; f < nrows; f += kStoreWaves * BATCH) {
+    for (int32_t f = f0; f < nrows; f += NS * BATCH) {
         const int32_t want = min(f + BATCH, nrows);
         if (avail < want) {
             int32_t sa = __builtin_amdgcn_readfirstlane(ctr_load(ctr));
-            if (sa != kDone && sa - 63 < want) sa = wait_counter(ctr, want + 63, A.ctrl);
-            avail = sa == kDone ? nrows : min(sa - 63, nrows);
+            if (sa != kDone && sa - 63 < want) sa = wait_counter(ctr, want + 63, A.ctrl, 8);
+            avail = (sa == kDone || sa == kDead) ? nrows : min(sa - 63, nrows);
+            lds_order();  // ring reads after the counter that released them
+            if (bcol) bnd0 = *bnd0p;
         }
         u32x4 v[NG];
 #pragma unroll
         for (int g = 0; g < NG; ++g) {
 #pragma unroll
             for (int m = 0; m < NR; ++m) {
-                const VT x = *(const VT *)(lds + pa[m]);
+                const VT x = *(const VT *)(ring + pa[m]);
                 pa[m] = adv(pa[m], NR);
 #pragma unroll
                 for (int k = 0; k < C; ++k) v[g][m * C + k] = (uint32_t)comp<C>(x, k);
             }
         }
 #pragma unroll
-        for (int m = 0; m < NR; ++m) pa[m] = adv(pa[m], (kStoreWaves - 1) * BATCH);  // skip the others'
-#if NW_BCAP > 0
-        // keep this CU's store queue short: the compute wave's hand-off polls
-        // wait behind it (vmcnt: vmcnt[3:0] | vmcnt[5:4] << 14, others maxed)
-        __builtin_amdgcn_s_waitcnt((NW_BCAP & 15) | (7 << 4) | (15 << 8) | ((NW_BCAP >> 4) << 14));
-#endif
+        for (int m = 0; m < NR; ++m) pa[m] = adv(pa[m], (NS - 1) * BATCH);  // skip the others'
         if (want - f == BATCH) {
 #pragma unroll
             for (int g = 0; g < NG; ++g)
@@ -626,18 +806,25 @@ __device__ void store_strip(const FillArgs &A, char *__restrict__ lds, int p, in
                 if (col_ok && f + g * NR + ro < nrows)
                     *(u32x4 *)(rowp + (int64_t)g * NR * rowb + voff) = v[g];
         }
-        rowp += kStoreWaves * BATCH * rowb;
-        ctr_store(mine, f + kStoreWaves * BATCH);  // my rows below are out of the ring
+        if (bcol) {
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {
+                const int32_t r = f + g * NR + ro;
+                if (cq == 0 && r < nrows)
+                    *(int32_t *)(rowp + (int64_t)g * NR * rowb + (int64_t)voff - 4) = bnd0 + r * A.gap;
+            }
+        }
+        rowp += NS * BATCH * rowb;
+        lds_order();
+        ctr_store(mine, f + NS * BATCH);  // my rows below are out of the ring
     }
     ctr_store(mine, kDone);
-    // Row band: hand this strip's columns of the last row (n2) to the next band.
+    // Row band: hand this ring's columns of the last row (n2) to the next band.
     // The table stores are plain (write-back L2), so: drain them, write the XCD's
     // L2 back (agent release), re-read the row with sc1 loads, publish
     // system-scope granules (write-through; peer HBM over xGMI when the next
-    // band lives on another GPU).
-    // (the store wave that stored row n2 does it)
-    if (A.halo_out != nullptr && ((nrows - 1) / BATCH) % kStoreWaves == b &&
-        ctrl_load(A.ctrl + 1) == 0u) {
+    // band lives on another GPU).  (The store wave that stored row n2 does it.)
+    if (A.halo_out != nullptr && ((nrows - 1) / BATCH) % NS == q && ctrl_load(A.ctrl + 1) == 0u) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         const int32_t *last = A.table + A.n2 * A.pitch;
@@ -651,66 +838,56 @@ __device__ void store_strip(const FillArgs &A, char *__restrict__ lds, int p, in
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
+        if (bcol && lane == 0)
+            __hip_atomic_store(A.halo_out,
+                               ((uint64_t)A.halo_tag << 32) | (uint32_t)(bnd0 + (int32_t)A.n2 * A.gap),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
-// Persistent grid of workgroups of 1 + kStoreWaves waves: wave 0 computes,
-// the others store.
-template <int C, bool UNIT>
-__global__ __launch_bounds__(64 * (1 + kStoreWaves)) void nw_fill_strips(FillArgs A) {
-    typedef Lay<C> L;
+// Persistent grid of workgroups of NC compute waves (0 .. NC-1) and NC*kSPR
+// store waves (wave NC + b serves ring b % NC).
+template <int C, int NC, bool UNIT>
+__global__ __launch_bounds__((64 * Lay<C, NC>::kWaves)) void nw_fill_strips(FillArgs A) {
+    typedef Lay<C, NC> L;
     __shared__ __attribute__((aligned(16))) char lds[L::kBytes];
-    int32_t *ctr = (int32_t *)(lds + L::kCtl);
+    int32_t *ctl = (int32_t *)(lds + L::kCtl);
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    // wave-uniform in an SGPR: every role / feed / output decision below is a
+    // scalar branch (a divergent one would run the untaken side's spin-waits
+    // with EXEC = 0, where they never see their counter)
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     for (;;) {
         if (threadIdx.x == 0) {
-            for (int b = 0; b < 1 + kStoreWaves; ++b) ctr[b] = 0;
-            ctr[3] = (int32_t)atomicAdd(A.ctrl, 1u);
+            for (int w = 0; w < L::kStripWord; ++w) ctl[w] = 0;
+            ctl[L::kStripWord] = (int32_t)atomicAdd(A.ctrl, 1u);
         }
         __syncthreads();
-        const int p = __builtin_amdgcn_readfirstlane(ctr[3]);
+        const int p = __builtin_amdgcn_readfirstlane(ctl[L::kStripWord]);
         if (p >= A.nstrips) break;
-        if (wave == 0) {
-            // profile form when the launch's profiles exist (nprof of them, built
-            // by nw_profile from the column characters), else the compares
+        if (wave < NC) {
+            // table form when the launch allows it (scores fit int8) and s1 has
+            // at most kMaxPerm distinct characters (nw_charmap), else compares
             const uint32_t np = __builtin_amdgcn_readfirstlane(ctrl_load(A.nprof));
-            if (A.prof != nullptr && np >= 1u && np <= kMaxProf)
-                compute_strip<C, SUB_PROF>(A, lds, p, lane);
+            if (A.perm != 0 && np <= kMaxPerm)
+                compute_strip<C, NC, SUB_PERM>(A, lds, p, wave, lane);
             else if (UNIT)
-                compute_strip<C, SUB_UNIT>(A, lds, p, lane);
+                compute_strip<C, NC, SUB_UNIT>(A, lds, p, wave, lane);
             else
-                compute_strip<C, SUB_GEN>(A, lds, p, lane);
-        } else
-            store_strip<C>(A, lds, p, lane, wave - 1);
-        __syncthreads();  // the ring and counters are reused by the next strip
+                compute_strip<C, NC, SUB_GEN>(A, lds, p, wave, lane);
+        } else {
+            const int b = wave - NC;
+            store_strip<C, NC>(A, lds, p, b % NC, b / NC, lane);
+        }
+        __syncthreads();  // the rings and counters are reused by the next strip
     }
-}
-
-// rowpack16[idx] = B[x .. x+15] (16 bytes), x = idx - kQOff, B[y] = s2[row0 + y - 1]
-// for 1 <= y <= n2 (local rows of this launch), else 0.
-__global__ void nw_rowpack(const uint8_t *__restrict__ s2, int64_t n2, int64_t row0,
-                           u32x4 *__restrict__ q, int64_t qlen) {
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= qlen) return;
-    const int64_t x = idx - kQOff;
-    u32x4 v = {0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const int64_t y = x + k;
-        const uint32_t b = (y >= 1 && y <= n2) ? (uint32_t)s2[row0 + y - 1] : 0u;
-        v[k >> 2] |= b << (8 * (k & 3));
-    }
-    q[idx] = v;
 }
 
 // Column-character map of a launch (one workgroup): which byte values occur in
-// s1, in increasing order -> charmap[c] = profile index (0xFF: absent),
-// chars[m] = the character of profile m (m < kMaxProf), *nprof = how many
-// distinct characters s1 holds.
+// s1, in increasing order -> charmap[c] = index (0xFF: absent), *nprof = how
+// many distinct characters s1 holds.
 __global__ __launch_bounds__(1024) void nw_charmap(const uint8_t *__restrict__ s1, int64_t n1,
                                                    uint8_t *__restrict__ charmap,
-                                                   uint8_t *__restrict__ chars,
                                                    uint32_t *__restrict__ nprof) {
     __shared__ uint32_t present[8];
     __shared__ uint32_t before[8];
@@ -739,88 +916,94 @@ __global__ __launch_bounds__(1024) void nw_charmap(const uint8_t *__restrict__ s
         const uint32_t idx = before[w] + (uint32_t)__builtin_popcount(present[w] & (bit - 1u));
         const bool here = (present[w] & bit) != 0u;
         charmap[c] = here ? (uint8_t)min(idx, 255u) : (uint8_t)0xFF;
-        if (here && idx < kMaxProf) chars[idx] = (uint8_t)c;
     }
 }
 
-// Query profiles (SUB_PROF): prof[m * qlen + idx] = 16 int8 of
-// s(chars[m], B[x + k]) - GAP, k < 16, x = idx - kQOff, B[y] = s2[row0 + y - 1]
-// for 1 <= y <= n2 (else 0) -- the rowpack16 layout with the substitution score
-// of column character chars[m] against every row already applied.
-__global__ void nw_profile(const uint8_t *__restrict__ s2, int64_t n2, int64_t row0,
-                           const uint8_t *__restrict__ chars, const uint32_t *__restrict__ nprof,
-                           int32_t match, int32_t mismatch, int32_t gap, u32x4 *__restrict__ prof,
-                           int64_t qlen) {
+// rowpack16[idx] = B[x .. x+15] (16 bytes), x = idx - kQOff, B[y] = s2[row0 + y - 1]
+// for 1 <= y <= n2 (local rows of this launch), else 0.  With `perm` set and
+// at most kMaxPerm distinct column characters (*nprof, from nw_charmap) the
+// bytes are MAPPED: charmap[B[y]], or 7 for a character in no column (and for
+// rows outside 1..n2) -- the SUB_PERM selector bytes.
+__global__ void nw_rowpack(const uint8_t *__restrict__ s2, int64_t n2, int64_t row0,
+                           const uint8_t *__restrict__ charmap, const uint32_t *__restrict__ nprof,
+                           int32_t perm, u32x4 *__restrict__ q, int64_t qlen) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t m = blockIdx.y;
-    if (idx >= qlen || m >= *nprof) return;
-    const uint32_t a = chars[m];
+    if (idx >= qlen) return;
+    const bool map = perm != 0 && *nprof <= kMaxPerm;
     const int64_t x = idx - kQOff;
     u32x4 v = {0u, 0u, 0u, 0u};
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
         const int64_t y = x + k;
-        const uint32_t b = (y >= 1 && y <= n2) ? (uint32_t)s2[row0 + y - 1] : 0u;
-        const uint32_t sc = (uint32_t)((a == b ? match : mismatch) - gap) & 255u;
-        v[k >> 2] |= sc << (8 * (k & 3));
+        uint32_t b = (y >= 1 && y <= n2) ? (uint32_t)s2[row0 + y - 1] : 0u;
+        if (map) b = (y >= 1 && y <= n2) ? min((uint32_t)charmap[b], 7u) : 7u;
+        v[k >> 2] |= b << (8 * (k & 3));
     }
-    prof[(int64_t)m * qlen + idx] = v;
+    q[idx] = v;
 }
 
-int launch_profiles(const uint8_t *d_s1, int64_t n1, const uint8_t *d_s2, int64_t n2,
-                    int64_t row0, int32_t match, int32_t mismatch, int32_t gap, uint8_t *meta,
-                    void *d_prof, int64_t qlen, void *stream) {
-    uint8_t *charmap = meta, *chars = meta + 256;
-    uint32_t *nprof = (uint32_t *)(meta + 256 + kMaxProf);
+// entries of 16 bytes: iteration j <= nblocks + 3 (prefetch of the last one)
+// reads up to index kQOff + 64 * (nblocks + 3) + 48
+int64_t rowpack_len(int32_t nblocks) { return kQOff + 64 * ((int64_t)nblocks + 4) + 16; }
+
+int launch_rowpack(const uint8_t *d_s1, int64_t n1, const uint8_t *d_s2, int64_t n2, int64_t row0,
+                   int32_t perm, uint8_t *meta, void *d_q, int64_t qlen, void *stream) {
+    uint8_t *charmap = meta;
+    uint32_t *nprof = (uint32_t *)(meta + 256);
     hipLaunchKernelGGL(nw_charmap, dim3(1), dim3(1024), 0, (hipStream_t)stream, d_s1, n1, charmap,
-                       chars, nprof);
+                       nprof);
     const int bs = 256;
     const int64_t nb = (qlen + bs - 1) / bs;
-    hipLaunchKernelGGL(nw_profile, dim3((unsigned)nb, kMaxProf), dim3(bs), 0, (hipStream_t)stream,
-                       d_s2, n2, row0, chars, nprof, match, mismatch, gap, (u32x4 *)d_prof, qlen);
+    hipLaunchKernelGGL(nw_rowpack, dim3((unsigned)nb), dim3(bs), 0, (hipStream_t)stream, d_s2, n2,
+                       row0, charmap, nprof, perm, (u32x4 *)d_q, qlen);
     return (int)hipGetLastError();
 }
 
-// entries of 16 bytes: iteration j <= nblocks + 2 (prefetch of the last one)
-// reads up to index kQOff + 64 * (nblocks + 2) + 48
-int64_t rowpack_len(int32_t nblocks) { return kQOff + 64 * ((int64_t)nblocks + 3) + 16; }
-
-int launch_rowpack(const uint8_t *d_s2, int64_t n2, int64_t row0, void *d_q, int64_t qlen,
-                   void *stream) {
-    const int bs = 256;
-    const int64_t nb = (qlen + bs - 1) / bs;
-    hipLaunchKernelGGL(nw_rowpack, dim3((unsigned)nb), dim3(bs), 0, (hipStream_t)stream, d_s2,
-                       n2, row0, (u32x4 *)d_q, qlen);
-    return (int)hipGetLastError();
-}
-
-template <int C>
+template <int C, int NC>
 static void launch_c(const FillArgs &a, int grid, hipStream_t s) {
+    const dim3 block(64 * Lay<C, NC>::kWaves);
     if (a.match - a.mismatch == 1)
-        hipLaunchKernelGGL((nw_fill_strips<C, true>), dim3(grid), dim3((1 + kStoreWaves) * kWave), 0, s, a);
+        hipLaunchKernelGGL((nw_fill_strips<C, NC, true>), dim3(grid), block, 0, s, a);
     else
-        hipLaunchKernelGGL((nw_fill_strips<C, false>), dim3(grid), dim3((1 + kStoreWaves) * kWave), 0, s, a);
+        hipLaunchKernelGGL((nw_fill_strips<C, NC, false>), dim3(grid), block, 0, s, a);
 }
 
-int launch_fill(const FillArgs &a, int substrips, int grid, void *stream) {
+// Supported (columns per lane, compute waves per strip) shapes.
+bool shape_ok(int substrips, int strip_waves) {
+    switch (substrips * 8 + strip_waves) {
+        case 4 * 8 + 1: case 2 * 8 + 1: case 1 * 8 + 1:
+        case 2 * 8 + 2: case 1 * 8 + 2: case 1 * 8 + 4:
+            return true;
+        default:
+            return false;
+    }
+}
+
+int launch_fill(const FillArgs &a, int substrips, int strip_waves, int grid, void *stream) {
     hipStream_t s = (hipStream_t)stream;
-    switch (substrips) {
-        case 1: launch_c<1>(a, grid, s); break;
-        case 2: launch_c<2>(a, grid, s); break;
-        case 4: launch_c<4>(a, grid, s); break;
+    switch (substrips * 8 + strip_waves) {
+        case 4 * 8 + 1: launch_c<4, 1>(a, grid, s); break;
+        case 2 * 8 + 1: launch_c<2, 1>(a, grid, s); break;
+        case 1 * 8 + 1: launch_c<1, 1>(a, grid, s); break;
+        case 2 * 8 + 2: launch_c<2, 2>(a, grid, s); break;
+        case 1 * 8 + 2: launch_c<1, 2>(a, grid, s); break;
+        case 1 * 8 + 4: launch_c<1, 4>(a, grid, s); break;
         default: return (int)hipErrorInvalidValue;
     }
     return (int)hipGetLastError();
 }
 
-int lds_bytes(int substrips) {
-    switch (substrips) {
-        case 1: return Lay<1>::kBytes;
-        case 2: return Lay<2>::kBytes;
-        default: return Lay<4>::kBytes;
+int lds_bytes(int substrips, int strip_waves) {
+    switch (substrips * 8 + strip_waves) {
+        case 4 * 8 + 1: return Lay<4, 1>::kBytes;
+        case 2 * 8 + 1: return Lay<2, 1>::kBytes;
+        case 1 * 8 + 1: return Lay<1, 1>::kBytes;
+        case 2 * 8 + 2: return Lay<2, 2>::kBytes;
+        case 1 * 8 + 2: return Lay<1, 2>::kBytes;
+        default: return Lay<1, 4>::kBytes;
     }
 }
 
-const char *kernel_variant() { return "strip-64xC-computewave+storewave-diagring-rowflush-gran64"; }
+const char *kernel_variant() { return "strip-NCx64xC-chained-computewaves+storewaves-diagring128-vperm-gran16"; }
 
 }  // namespace nw

@@ -11,8 +11,8 @@ constexpr int32_t kNeg = -(1 << 29);  // "minus infinity" fed left of column 0
 constexpr int kScratchWords = kWave * kWave + 2 * kWave;  // per workgroup (16.5 KB)
 constexpr int kMaxSub = 4;        // max columns per lane (strip = 64 * C columns)
 constexpr int kTraceWords = 16;    // debug trace words per strip
-constexpr uint32_t kMaxProf = 16;  // query profiles per launch (distinct column characters)
-constexpr int kMetaBytes = 256 + kMaxProf + 16;  // charmap[256], chars[kMaxProf], nprof
+constexpr uint32_t kMaxPerm = 7;  // distinct column characters the v_perm score tables cover
+constexpr int kMetaBytes = 256 + 16;  // charmap[256], nprof (+ pad)
 
 // Everything one launch of the strip-sweep kernel needs.  Plain POD, passed by
 // value as the kernel argument.
@@ -20,17 +20,20 @@ struct FillArgs {
     int32_t *table;            // device table, row-major, row pitch `pitch` (int32 elems)
     int64_t pitch;             // multiple of 64 (256-B aligned rows)
     const void *rowpack;       // 16-byte entries: rowpack[x + kQOff] = B[x .. x+15],
-                               //   B[x] = s2[x-1] for 1 <= x <= n2, else 0
+                               //   B[x] = s2[x-1] for 1 <= x <= n2, else 0 (raw or
+                               //   mapped through charmap: nw_rowpack)
     const uint8_t *s1;         // n1 column characters
     int64_t n1, n2;            // nCols = n1 + 1, nRows = n2 + 1
     int64_t row0;              // global row index of local row 0 (0 for a whole table)
-    int32_t nstrips;           // super-strips: ceil(nCols / (64 * substrips))
+    int64_t col0;              // first swept column: 1 when column 1 starts a 256-B line
+                               //   (column 0 = the boundary, stored separately), else 0
+    int32_t nstrips;           // strips: ceil((nCols - col0) / (strip_waves * 64 * substrips))
     int32_t nblocks;           // ceil(nRows / 64)
     uint64_t *gran;            // right-boundary hand-off granules [M][gstride] {tag:32 | value:32}
     int64_t gstride;           // granules per slot = 64 * nblocks
     int32_t M;                 // number of slots (>= waves + 1, or nstrips)
     uint32_t tagbase;          // strip p publishes tag tagbase + p + 1
-    uint32_t *ctrl;            // [0] strip ticket, [1] error word, [2..3] spare
+    uint32_t *ctrl;            // [0] strip ticket, [1] error word, [2..4] watchdog site/need/seen
     // Row bands (mpi-horz contract): row 0 of this launch is the previous band's
     // last row, delivered as granules {tag:32 | value:32}, one per column 0..n1.
     const uint64_t *halo_in;   // NULL = row 0 is the boundary j*gap (first band / whole table)
@@ -38,11 +41,10 @@ struct FillArgs {
     uint32_t halo_tag;         // launch tag shared with the neighbouring bands (> 0)
     int32_t *scratch;          // per-workgroup dummy flush target: grid * kScratchWords int32
     uint64_t *trace;           // optional per-strip debug trace [nstrips][kTraceWords]
-    // Query profiles (NULL = compare form): kMaxProf profiles of prof_stride
-    // 16-byte entries (rowpack16 layout, int8 s(c, row) - GAP), the character
-    // map of s1 and the count, all written on the device by launch_profiles.
-    const void *prof;
-    int64_t prof_stride;
+    // v_perm score tables (SUB_PERM): allowed by the host when s - GAP fits
+    // int8 for both scores; used when s1 has <= kMaxPerm distinct characters.
+    // charmap / nprof are written on the device by launch_rowpack (nw_charmap).
+    int32_t perm;
     const uint8_t *charmap;
     const uint32_t *nprof;
     int32_t match, mismatch, gap;
@@ -50,13 +52,12 @@ struct FillArgs {
 };
 
 // Launch helpers implemented in nw_fill.hip.  Return hipError_t as int.
-int launch_rowpack(const uint8_t *d_s2, int64_t n2, int64_t row0, void *d_q, int64_t qlen,
-                   void *stream);
-int launch_profiles(const uint8_t *d_s1, int64_t n1, const uint8_t *d_s2, int64_t n2,
-                    int64_t row0, int32_t match, int32_t mismatch, int32_t gap, uint8_t *meta,
-                    void *d_prof, int64_t qlen, void *stream);
-int launch_fill(const FillArgs &a, int substrips, int grid, void *stream);
-int lds_bytes(int substrips);
+// charmap of s1 into meta, then the row packs (mapped when perm allows it)
+int launch_rowpack(const uint8_t *d_s1, int64_t n1, const uint8_t *d_s2, int64_t n2, int64_t row0,
+                   int32_t perm, uint8_t *meta, void *d_q, int64_t qlen, void *stream);
+bool shape_ok(int substrips, int strip_waves);
+int launch_fill(const FillArgs &a, int substrips, int strip_waves, int grid, void *stream);
+int lds_bytes(int substrips, int strip_waves);
 int64_t rowpack_len(int32_t nblocks);  // 16-byte entries
 const char *kernel_variant();
 

@@ -39,18 +39,12 @@ def plan(n2: int, nbands: int):
     return [nwhip.band_layout(n2, nbands, r) for r in range(nbands)]
 
 
-# LDS ring slots per strip workgroup by columns per lane (nw_fill.hip, Lay<C>::R)
-RING_SLOTS = {1: 148, 2: 152, 4: 76}
-
-
-def resident_waves(device: int = 0, substrips: int = 2) -> int:
-    """Persistent strip workers (workgroups) that fit on the device at once
-    (LDS-bound: the ring of R slots x 64*C int32 + two feed buffers + counters,
-    as nw::lds_bytes)."""
+def resident_waves(device: int = 0, substrips: int = 2, strip_waves: int = 2) -> int:
+    """Persistent strip workgroups that fit on the device at once (LDS-bound:
+    nw_strip_lds_bytes per workgroup, 160 KiB per CU)."""
     import torch
     cus = torch.cuda.get_device_properties(device).multi_processor_count
-    lds = substrips * 64 * 4 * RING_SLOTS[substrips] + 2 * 64 * 4 + 16
-    return cus * (LDS_PER_CU // lds)
+    return cus * (LDS_PER_CU // nwhip.strip_lds_bytes(*nwhip.strip_shape(substrips, strip_waves)))
 
 
 class LocalBands:
@@ -59,10 +53,12 @@ class LocalBands:
     Each band gets at most 1/P of the resident workers so that all bands are
     co-resident (a band waiting for its halo never blocks its producer)."""
 
-    def __init__(self, n1: int, n2: int, nbands: int, device: int = 0, substrips: int = 2):
+    def __init__(self, n1: int, n2: int, nbands: int, device: int = 0, substrips: int = 2,
+                 strip_waves: int = 2):
         import torch
         self.n1, self.n2, self.P, self.device = n1, n2, nbands, device
         self.substrips = substrips
+        self.strip_waves = strip_waves
         self.layout = plan(n2, nbands)
         if any(rows < 1 for rows, _ in self.layout):
             raise ValueError(f"{nbands} bands need at least {nbands} rows (n2+1 = {n2 + 1})")
@@ -70,7 +66,7 @@ class LocalBands:
         self.halos = [None] + [nwhip.Halo(n1, device) for _ in range(nbands - 1)]
         self.ctxs = [nwhip.Context(device) for _ in range(nbands)]
         self.streams = [torch.cuda.Stream(device) for _ in range(nbands)]
-        self.waves = max(1, resident_waves(device, substrips) // nbands)
+        self.waves = max(1, resident_waves(device, substrips, strip_waves) // nbands)
         self.tag = 0
 
     def fill(self, d_s1, d_s2, scheme=(1, 0, -1), flags: int = 0) -> int:
@@ -86,7 +82,7 @@ class LocalBands:
                 halo_in=self.halos[r].ptr if r > 0 else None,
                 halo_out=self.halos[r + 1].ptr if r + 1 < self.P else None,
                 tag=self.tag, scheme=scheme, waves=self.waves, stream=st, flags=flags,
-                substrips=self.substrips)
+                substrips=self.substrips, strip_waves=self.strip_waves)
         for r, st in enumerate(self.streams):
             s = self.ctxs[r].status(st)
             if s != nwhip.NW_OK:
@@ -154,7 +150,7 @@ def run_bands(args) -> dict | None:
     halo_out = nwhip.ipc_open_handle(handles[rank + 1]) if rank + 1 < world else None
     waves = args.waves
     if args.share_gpu and waves == 0:
-        waves = max(1, resident_waves(dev, 1) // world)
+        waves = max(1, resident_waves(dev, args.substrips, args.strip_waves) // world)
     stream = torch.cuda.current_stream()
     tag = 0
 
@@ -165,7 +161,7 @@ def run_bands(args) -> dict | None:
             ev[0].record(stream)
         ctx.fill_band(s1, s2_band, table, halo_in=halo_in.ptr if halo_in else None,
                       halo_out=halo_out, tag=tag, scheme=scheme, waves=waves, stream=stream,
-                      substrips=args.substrips)
+                      substrips=args.substrips, strip_waves=args.strip_waves)
         if ev is not None:
             ev[1].record(stream)
         torch.cuda.synchronize()

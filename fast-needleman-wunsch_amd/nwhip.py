@@ -25,7 +25,7 @@ NW_OK, NW_ERR_ARG, NW_ERR_HIP, NW_ERR_OOM, NW_ERR_TIMEOUT, NW_ERR_NODEVICE, NW_E
 
 # every symbol include/nw_hip.h declares (checked by tests/test_host.py)
 EXPORTS = ["nw_params_default", "nw_strerror", "nw_version", "nw_fill", "nw_table_pitch",
-           "nw_table_bytes", "nw_ctx_create", "nw_ctx_destroy", "nw_ctx_workspace_bytes",
+           "nw_table_bytes", "nw_table_offset", "nw_strip_lds_bytes", "nw_ctx_create", "nw_ctx_destroy", "nw_ctx_workspace_bytes",
            "nw_fill_device", "nw_fill_device_async", "nw_ctx_status", "nw_read_bdna", "nw_free",
            "nw_synth_bdna", "nw_band_layout", "nw_halo_bytes", "nw_fill_band_async",
            "nw_ipc_get_handle", "nw_ipc_open_handle", "nw_ipc_close_handle", "nw_halo_alloc",
@@ -36,14 +36,15 @@ IPC_HANDLE_BYTES = 64
 class NwParams(ctypes.Structure):
     _fields_ = [("match", ctypes.c_int32), ("mismatch", ctypes.c_int32), ("gap", ctypes.c_int32),
                 ("mode", ctypes.c_int32), ("waves", ctypes.c_int32), ("device", ctypes.c_int32),
-                ("flags", ctypes.c_int32), ("substrips", ctypes.c_int32)]
+                ("flags", ctypes.c_int32), ("substrips", ctypes.c_int32),
+                ("strip_waves", ctypes.c_int32)]
 
 
 class NwResult(ctypes.Structure):
     _fields_ = [("score", ctypes.c_int32), ("status", ctypes.c_int32), ("cells", ctypes.c_int64),
                 ("kernel_ms", ctypes.c_double), ("table_bytes", ctypes.c_double),
                 ("strips", ctypes.c_int32), ("waves", ctypes.c_int32),
-                ("substrips", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("substrips", ctypes.c_int32), ("strip_waves", ctypes.c_int32)]
 
 
 class NwBand(ctypes.Structure):
@@ -91,6 +92,10 @@ def lib() -> ctypes.CDLL:
     L.nw_table_pitch.restype = ctypes.c_int64
     L.nw_table_bytes.argtypes = [ctypes.c_int64, ctypes.c_int64]
     L.nw_table_bytes.restype = ctypes.c_int64
+    L.nw_table_offset.argtypes = []
+    L.nw_table_offset.restype = ctypes.c_int64
+    L.nw_strip_lds_bytes.argtypes = [ctypes.c_int32, ctypes.c_int32]
+    L.nw_strip_lds_bytes.restype = ctypes.c_int64
     L.nw_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
     L.nw_ctx_destroy.argtypes = [ctypes.c_void_p]
     L.nw_ctx_destroy.restype = None
@@ -144,7 +149,7 @@ class Scheme:
 
 
 def params(scheme=(1, 0, -1), waves: int = 0, device: int = -1, flags: int = 0,
-           substrips: int = 0) -> NwParams:
+           substrips: int = 0, strip_waves: int = 0) -> NwParams:
     if isinstance(scheme, Scheme):
         scheme = (scheme.match, scheme.mismatch, scheme.gap)
     p = NwParams()
@@ -154,6 +159,7 @@ def params(scheme=(1, 0, -1), waves: int = 0, device: int = -1, flags: int = 0,
     p.device = int(device)
     p.flags = int(flags)
     p.substrips = int(substrips)
+    p.strip_waves = int(strip_waves)
     return p
 
 
@@ -167,12 +173,12 @@ FLAG_TIMING_ONLY, FLAG_NO_PROFILE = 1, 2  # nw_params.flags (include/nw_hip.h)
 
 
 def fill(s1, s2, scheme=(1, 0, -1), waves: int = 0, device: int = -1, substrips: int = 0,
-         flags: int = 0):
+         flags: int = 0, strip_waves: int = 0):
     """Full table in the reference layout ((n2+1) x (n1+1) int32) + NwResult."""
     a, b = _seq(s1), _seq(s2)
     t = np.empty((b.size + 1, a.size + 1), dtype=np.int32)
     r = NwResult()
-    p = params(scheme, waves, device, flags=flags, substrips=substrips)
+    p = params(scheme, waves, device, flags=flags, substrips=substrips, strip_waves=strip_waves)
     st = lib().nw_fill(a.ctypes.data_as(_i8p), a.size, b.ctypes.data_as(_i8p), b.size,
                        ctypes.byref(p), t.ctypes.data_as(_i32p), ctypes.byref(r))
     if st != NW_OK:
@@ -180,10 +186,11 @@ def fill(s1, s2, scheme=(1, 0, -1), waves: int = 0, device: int = -1, substrips:
     return t, r
 
 
-def score(s1, s2, scheme=(1, 0, -1), waves: int = 0, device: int = -1, substrips: int = 0) -> int:
+def score(s1, s2, scheme=(1, 0, -1), waves: int = 0, device: int = -1, substrips: int = 0,
+          strip_waves: int = 0) -> int:
     a, b = _seq(s1), _seq(s2)
     r = NwResult()
-    p = params(scheme, waves, device, substrips=substrips)
+    p = params(scheme, waves, device, substrips=substrips, strip_waves=strip_waves)
     st = lib().nw_fill(a.ctypes.data_as(_i8p), a.size, b.ctypes.data_as(_i8p), b.size,
                        ctypes.byref(p), None, ctypes.byref(r))
     if st != NW_OK:
@@ -197,6 +204,28 @@ def table_pitch(n1: int) -> int:
 
 def table_rows(n2: int) -> int:
     return (n2 + 1 + 63) // 64 * 64
+
+
+def table_offset() -> int:
+    """Element offset of the table base from a 256-byte aligned allocation that
+    puts column 1 on a 256-byte line (nw_table_offset)."""
+    return int(lib().nw_table_offset())
+
+
+def strip_shape(substrips: int = 0, strip_waves: int = 0) -> tuple[int, int]:
+    """(C, NC) the library uses for these nw_params values (0 = auto), as
+    make_shape in nw_capi.cpp: auto = (2, 2); C alone implies 256-column strips."""
+    c = substrips if substrips > 0 else 2
+    if strip_waves > 0:
+        return c, strip_waves
+    if substrips > 0:
+        return c, {1: 4, 2: 2, 4: 1}[c]
+    return c, 2
+
+
+def strip_lds_bytes(substrips: int, strip_waves: int) -> int:
+    """LDS bytes of one strip workgroup of this shape (-1: unsupported shape)."""
+    return int(lib().nw_strip_lds_bytes(substrips, strip_waves))
 
 
 def read_bdna(path: str) -> np.ndarray:
@@ -297,22 +326,33 @@ class Context:
             pass
 
     @staticmethod
-    def alloc_table(n1: int, n2: int, device="cuda"):
+    def alloc_table(n1: int, n2: int, device="cuda", pitch: int = 0):
+        """(table_rows(n2), table_pitch(n1)) int32 view whose base sits
+        table_offset() elements into a 256-byte aligned allocation, so that column
+        1 of every row starts a 256-byte line (the fill then sweeps columns 1..n1
+        in whole strips; include/nw_hip.h, nw_table_offset).  `pitch` (a
+        multiple of 64 >= table_pitch(n1)) overrides the row pitch."""
         import torch
-        return torch.empty((table_rows(n2), table_pitch(n1)), dtype=torch.int32, device=device)
+        rows = table_rows(n2)
+        pitch = pitch or table_pitch(n1)
+        assert pitch % 64 == 0 and pitch >= table_pitch(n1)
+        off = table_offset() if n1 >= 1 else 0  # (no column 1 when n1 = 0)
+        flat = torch.empty(rows * pitch + 64, dtype=torch.int32, device=device)
+        shift = (-(flat.data_ptr() // 4) + off) % 64  # torch allocations are 512-B aligned
+        return flat[shift:shift + rows * pitch].view(rows, pitch)
 
     def fill(self, d_s1, d_s2, table, scheme=(1, 0, -1), waves: int = 0, stream=None,
-             sync: bool = True, flags: int = 0, substrips: int = 0):
+             sync: bool = True, flags: int = 0, substrips: int = 0, strip_waves: int = 0):
         """d_s1/d_s2: int8/uint8 CUDA tensors; table: from alloc_table.  Returns NwResult
         when sync, else None (launch only)."""
         import torch
         n1, n2 = int(d_s1.numel()), int(d_s2.numel())
         assert table.dtype == torch.int32 and table.is_contiguous()
-        assert table.shape[0] >= table_rows(n2) and table.shape[1] == table_pitch(n1)
+        assert table.shape[0] >= table_rows(n2) and table.shape[1] >= n1 + 1 and table.shape[1] % 64 == 0
         if stream is None:
             stream = torch.cuda.current_stream(table.device)
         sp = ctypes.c_void_p(stream.cuda_stream)
-        p = params(scheme, waves, self.device, flags, substrips)
+        p = params(scheme, waves, self.device, flags, substrips, strip_waves)
         args = (self._h, ctypes.c_void_p(d_s1.data_ptr() if n1 else 0), n1,
                 ctypes.c_void_p(d_s2.data_ptr() if n2 else 0), n2, ctypes.byref(p),
                 ctypes.c_void_p(table.data_ptr()), table.shape[1], sp)
@@ -329,7 +369,7 @@ class Context:
 
     def fill_band(self, d_s1, d_s2_band, table, halo_in=None, halo_out=None, tag: int = 1,
                   scheme=(1, 0, -1), waves: int = 0, stream=None, flags: int = 0,
-                  substrips: int = 0) -> None:
+                  substrips: int = 0, strip_waves: int = 0) -> None:
         """Launch one row band (asynchronous).  d_s2_band: the band's side
         characters (len = band rows - 1); table: alloc_table(n1, len(d_s2_band)),
         row 0 = the halo row.  halo_in / halo_out: int64 CUDA tensors of
@@ -337,7 +377,7 @@ class Context:
         import torch
         n1, n2 = int(d_s1.numel()), int(d_s2_band.numel())
         assert table.dtype == torch.int32 and table.is_contiguous()
-        assert table.shape[0] >= table_rows(n2) and table.shape[1] == table_pitch(n1)
+        assert table.shape[0] >= table_rows(n2) and table.shape[1] >= n1 + 1 and table.shape[1] % 64 == 0
 
         def addr(x):
             if x is None:
@@ -349,7 +389,7 @@ class Context:
         if stream is None:
             stream = torch.cuda.current_stream(table.device)
         b = NwBand(addr(halo_in), addr(halo_out), int(tag), 0)
-        p = params(scheme, waves, self.device, flags, substrips)
+        p = params(scheme, waves, self.device, flags, substrips, strip_waves)
         st = lib().nw_fill_band_async(self._h, ctypes.c_void_p(d_s1.data_ptr() if n1 else 0), n1,
                                       ctypes.c_void_p(d_s2_band.data_ptr() if n2 else 0), n2,
                                       ctypes.byref(p), ctypes.byref(b),

@@ -46,7 +46,8 @@ enum { NW_MODE_NW = 0 };
 /* nw_params.flags (0 = normal fill) */
 enum {
     NW_FLAG_TIMING_ONLY = 1, /* table stores go to a scratch tile (kernel timing only) */
-    NW_FLAG_NO_PROFILE = 2   /* substitution by byte compares instead of query profiles */
+    NW_FLAG_NO_PROFILE = 2   /* substitution by byte compares instead of the per-lane
+                                v_perm score tables */
 };
 
 /* Runtime replacement for the compile-time constants of
@@ -59,7 +60,10 @@ typedef struct nw_params {
     int32_t waves;     /* persistent strip workers (waves; 0 = auto)     */
     int32_t device;    /* HIP device ordinal, -1 = current device         */
     int32_t flags;     /* NW_FLAG_* bits, 0 for a normal fill            */
-    int32_t substrips; /* 64-column sub-strips per wave (1, 2 or 4); 0 = auto */
+    int32_t substrips; /* columns per lane C of a compute wave (1, 2 or 4); 0 = auto */
+    int32_t strip_waves; /* chained compute waves per strip NC (1, 2 or 4); 0 = auto.
+                            A strip is NC * 64 * C columns; supported (C, NC):
+                            (4,1) (2,1) (1,1) (2,2) (1,2) (1,4); auto = (2,2) */
 } nw_params;
 
 typedef struct nw_result {
@@ -70,8 +74,8 @@ typedef struct nw_result {
     double table_bytes;     /* bytes of table stored: 4 * nRows * nCols   */
     int32_t strips;         /* super-strips swept (substrips*64 columns)  */
     int32_t waves;          /* persistent workers launched                */
-    int32_t substrips;      /* 64-column sub-strips per wave              */
-    int32_t reserved;
+    int32_t substrips;      /* columns per lane of a compute wave         */
+    int32_t strip_waves;    /* compute waves per strip                    */
 } nw_result;
 
 /* Fill `p` with the reference defaults (1, 0, -1). */
@@ -97,12 +101,27 @@ int nw_fill(const int8_t *s1, int64_t n1, const int8_t *s2, int64_t n2,
 /* Device-resident API ------------------------------------------------------ */
 typedef struct nw_ctx nw_ctx;
 
-/* Row pitch (in int32 elements) the device kernel requires for nCols = n1+1:
- * a multiple of 64 (256-byte aligned rows). */
+/* Row pitch (in int32 elements) the library allocates for nCols = n1+1: a
+ * multiple of 64 (256-byte rows) with at least 3 columns of slack after column
+ * n1, which the strips need to start at column 1 (nw_table_offset).  Any
+ * multiple of 64 >= n1 + 1 is accepted; a tighter one sweeps from column 0. */
 int64_t nw_table_pitch(int64_t n1);
 
 /* Bytes of device memory a table of (n2+1) rows at nw_table_pitch(n1) takes. */
 int64_t nw_table_bytes(int64_t n1, int64_t n2);
+
+/* Preferred element offset of the table base from a 256-byte aligned
+ * allocation (of nw_table_bytes + 256 bytes): 63, which puts column 1 of every
+ * row on a 256-byte line.  The fill then sweeps columns 1..n1 only -- an
+ * N x N table is exactly N / 256 strips -- and stores the boundary column 0
+ * separately.  A 256-byte aligned base (offset 0) is accepted too. */
+int64_t nw_table_offset(void);
+
+/* LDS bytes of one strip workgroup of shape (C = substrips, NC = strip_waves),
+ * -1 for an unsupported shape.  A CU holds floor(160 KiB / this) of them; a
+ * caller co-scheduling several fills on one device (LocalBands) sizes their
+ * `waves` from it so that all of them stay resident. */
+int64_t nw_strip_lds_bytes(int32_t substrips, int32_t strip_waves);
 
 /* Create / destroy a context bound to `device` (-1 = current).  The context
  * owns the hand-off workspace and the strip ticket counter. */
@@ -114,8 +133,10 @@ int64_t nw_ctx_workspace_bytes(int64_t n1, int64_t n2, int32_t waves);
 
 /*
  * Fill a device-resident table.  d_s1/d_s2: device int8 sequences; d_t: device
- * table with row pitch `pitch` (>= nw_table_pitch(n1), multiple of 64,
- * 256-byte aligned base).  `stream` is a hipStream_t (NULL = default stream).
+ * table with row pitch `pitch` (a multiple of 64 >= n1 + 1; nw_table_pitch
+ * preferred), base 256-byte aligned or -- preferred -- 4 bytes short of it
+ * (nw_table_offset; used when pitch >= n1 + 4).
+ * `stream` is a hipStream_t (NULL = default stream).
  * Asynchronous with respect to the host unless out != NULL, in which case the
  * call synchronises the stream and fills `out` (score read back from HBM).
  */

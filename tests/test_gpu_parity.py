@@ -34,11 +34,28 @@ def ctx(torch):
     c.close()
 
 
-def device_fill(torch, ctx, s1, s2, scheme=(1, 0, -1), waves=0, substrips=0):
+# every supported (columns per lane C, compute waves per strip NC)
+STRIP_SHAPES = [(4, 1), (2, 1), (1, 1), (2, 2), (1, 2), (1, 4)]
+
+
+def alloc_aligned_table(torch, n1, n2):
+    """A table whose base is 256-byte aligned (strip origin column 0: the boundary
+    column is swept like any other), instead of alloc_table's column-1 alignment."""
+    rows, pitch = nwhip.table_rows(n2), nwhip.table_pitch(n1)
+    flat = torch.empty(rows * pitch + 64, dtype=torch.int32, device="cuda")
+    shift = (-(flat.data_ptr() // 4)) % 64
+    return flat[shift:shift + rows * pitch].view(rows, pitch)
+
+
+def device_fill(torch, ctx, s1, s2, scheme=(1, 0, -1), waves=0, substrips=0, strip_waves=0,
+                col0=1):
     d1 = torch.from_numpy(np.ascontiguousarray(s1)).cuda()
     d2 = torch.from_numpy(np.ascontiguousarray(s2)).cuda()
-    tab = nwhip.Context.alloc_table(s1.size, s2.size)
-    r = ctx.fill(d1, d2, tab, scheme, waves=waves, substrips=substrips)
+    if col0 == 1:
+        tab = nwhip.Context.alloc_table(s1.size, s2.size)
+    else:
+        tab = alloc_aligned_table(torch, s1.size, s2.size)
+    r = ctx.fill(d1, d2, tab, scheme, waves=waves, substrips=substrips, strip_waves=strip_waves)
     assert r.status == 0
     return tab, r
 
@@ -95,29 +112,48 @@ SHAPES = [(0, 0), (0, 1), (1, 0), (1, 1), (2, 3), (63, 63), (64, 64), (65, 65), 
 
 @pytest.mark.parametrize("shape", SHAPES)
 @pytest.mark.parametrize("alphabet", ["dna", "bytes"])
-@pytest.mark.parametrize("substrips", [1, 2, 4])
-@pytest.mark.parametrize("form", ["profile", "compare"])
-def test_random_vs_oracle(shape, alphabet, substrips, form):
-    """Both substitution forms: query profiles (default; the "bytes" alphabet has
-    more distinct column characters than profiles and falls back on the device)
-    and byte compares (NW_FLAG_NO_PROFILE)."""
+@pytest.mark.parametrize("strip", STRIP_SHAPES)
+@pytest.mark.parametrize("form", ["table", "compare"])
+def test_random_vs_oracle(shape, alphabet, strip, form):
+    """Both substitution forms: per-lane v_perm score tables (default; the "bytes"
+    alphabet has more distinct column characters than a table covers and falls
+    back on the device) and byte compares (NW_FLAG_NO_PROFILE), for every strip
+    shape (C columns per lane, NC chained compute waves)."""
     rng = np.random.default_rng(shape[0] * 7919 + shape[1] + (alphabet == "bytes"))
     lo, hi = (1, 5) if alphabet == "dna" else (-128, 128)
     s1 = rng.integers(lo, hi, shape[0]).astype(np.int8)
     s2 = rng.integers(lo, hi, shape[1]).astype(np.int8)
     flags = nwhip.FLAG_NO_PROFILE if form == "compare" else 0
     for scheme in SCHEMES.values():
-        t, r = nwhip.fill(s1, s2, scheme, substrips=substrips, flags=flags)
-        assert r.substrips == substrips
+        t, r = nwhip.fill(s1, s2, scheme, substrips=strip[0], strip_waves=strip[1], flags=flags)
+        assert (r.substrips, r.strip_waves) == strip
         np.testing.assert_array_equal(t, oracle.fill(s1, s2, scheme),
-                                      err_msg=str((shape, scheme, substrips, form)))
+                                      err_msg=str((shape, scheme, strip, form)))
 
 
-@pytest.mark.parametrize("ndistinct", [1, 2, 15, 16, 17, 40])
-def test_profile_count_boundary(ndistinct):
-    """Up to 16 distinct column characters use query profiles, more fall back to
-    compares inside the kernel; the table is the same either way.  Row characters
-    outside the column alphabet (never matching) are included."""
+@pytest.mark.parametrize("shape", [(0, 5), (1, 1), (63, 70), (255, 300), (256, 256), (257, 100),
+                                   (511, 77), (1000, 333)])
+@pytest.mark.parametrize("strip", STRIP_SHAPES)
+def test_strip_origin_column0(torch, ctx, shape, strip):
+    """A 256-byte aligned table base sweeps column 0 with the strips (origin 0);
+    alloc_table's base (column 1 aligned) stores the boundary column apart
+    (origin 1).  Both give the reference table."""
+    rng = np.random.default_rng(shape[0] + 31 * shape[1])
+    s1 = rng.integers(1, 5, shape[0]).astype(np.int8)
+    s2 = rng.integers(1, 5, shape[1]).astype(np.int8)
+    for col0 in (0, 1):
+        for scheme in [(1, 0, -1), (2, -1, -2)]:
+            tab, r = device_fill(torch, ctx, s1, s2, scheme, substrips=strip[0],
+                                 strip_waves=strip[1], col0=col0)
+            np.testing.assert_array_equal(tab[:s2.size + 1, :s1.size + 1].cpu().numpy(),
+                                          oracle.fill(s1, s2, scheme), err_msg=str((col0, scheme)))
+
+
+@pytest.mark.parametrize("ndistinct", [1, 2, 6, 7, 8, 40])
+def test_table_count_boundary(ndistinct):
+    """Up to 7 distinct column characters use the v_perm score tables, more fall
+    back to compares inside the kernel; the table is the same either way.  Row
+    characters outside the column alphabet (never matching) are included."""
     rng = np.random.default_rng(ndistinct)
     alphabet = rng.choice(np.arange(-128, 128), ndistinct, replace=False)
     s1 = rng.choice(alphabet, 900).astype(np.int8)
@@ -142,15 +178,16 @@ def test_other_schemes_vs_oracle(scheme):
 
 
 @pytest.mark.parametrize("waves", [1, 2, 3, 5, 8, 17, 64])
-@pytest.mark.parametrize("substrips", [1, 2, 4])
-def test_worker_count_independent(torch, ctx, waves, substrips):
+@pytest.mark.parametrize("strip", STRIP_SHAPES)
+def test_worker_count_independent(torch, ctx, waves, strip):
     """Few persistent workers -> many strips per worker and hand-off slot reuse
     (slot = strip % (waves + 1)); results must not depend on it."""
     rng = np.random.default_rng(waves)
     s1 = rng.integers(1, 5, 64 * 40 + 17).astype(np.int8)
     s2 = rng.integers(1, 5, 900).astype(np.int8)
     want = oracle.fill(s1, s2, (1, -1, -1))
-    tab, r = device_fill(torch, ctx, s1, s2, (1, -1, -1), waves=waves, substrips=substrips)
+    tab, r = device_fill(torch, ctx, s1, s2, (1, -1, -1), waves=waves, substrips=strip[0],
+                         strip_waves=strip[1])
     np.testing.assert_array_equal(tab[:s2.size + 1, :s1.size + 1].cpu().numpy(), want)
     assert r.waves == min(waves, r.strips)
 
@@ -167,13 +204,13 @@ def test_repeated_launches_and_shapes(torch, ctx):
         np.testing.assert_array_equal(tab[:n2 + 1, :n1 + 1].cpu().numpy(), oracle.fill(s1, s2))
 
 
-@pytest.mark.parametrize("substrips", [1, 2, 4])
-def test_config2_32k_vs_oracle(torch, ctx, substrips):
+@pytest.mark.parametrize("strip", [(4, 1), (2, 1), (2, 2), (1, 4)])
+def test_config2_32k_vs_oracle(torch, ctx, strip):
     """BASELINE config 2: 32k x 32k synthetic (seeds 1, 2), full table in HBM;
     every row checked through (sum, weighted sum), last row/column exactly."""
     n = 32768
     s1, s2 = nwhip.synth(1, n), nwhip.synth(2, n)
-    tab, r = device_fill(torch, ctx, s1, s2, (1, 0, -1), substrips=substrips)
+    tab, r = device_fill(torch, ctx, s1, s2, (1, 0, -1), substrips=strip[0], strip_waves=strip[1])
     sc, lr, lc, rs, rw = oracle.score(s1, s2, (1, 0, -1), want_rows=True)
     assert r.score == sc
     np.testing.assert_array_equal(tab[n, :n + 1].cpu().numpy(), lr)

@@ -49,10 +49,27 @@ def test_dropin_driver_exports_reference_plugin_symbol():
 
 
 def test_pitch_and_bytes():
+    # multiple of 64 holding nCols = n1 + 1 plus 3 columns of slack (the 16-byte
+    # store holding column n1 must stay inside the row when strips start at column 1)
     assert nwhip.table_pitch(0) == 64
-    assert nwhip.table_pitch(63) == 64
+    assert nwhip.table_pitch(60) == 64
+    assert nwhip.table_pitch(61) == 128
+    assert nwhip.table_pitch(63) == 128
     assert nwhip.table_pitch(64) == 128
+    assert nwhip.table_pitch(262144) == 262208
     assert nwhip.lib().nw_table_bytes(262144, 262144) == (262145 + 63) // 64 * 64 * 262208 * 4
+    assert nwhip.table_offset() == 63  # column 1 of every row on a 256-byte line
+
+
+def test_strip_shapes_lds():
+    """Every supported strip shape fits a CU's 160 KiB of LDS; others are refused."""
+    for c, nc in [(4, 1), (2, 1), (1, 1), (2, 2), (1, 2), (1, 4)]:
+        b = nwhip.strip_lds_bytes(c, nc)
+        assert 0 < b <= 160 * 1024, (c, nc, b)
+    assert nwhip.strip_lds_bytes(4, 2) == -1 and nwhip.strip_lds_bytes(3, 1) == -1
+    assert nwhip.strip_shape() == (2, 2)
+    assert nwhip.strip_shape(4) == (4, 1) and nwhip.strip_shape(1) == (1, 4)
+    assert nwhip.strip_shape(2, 1) == (2, 1)
 
 
 def test_default_params_are_reference_constants():

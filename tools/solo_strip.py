@@ -13,20 +13,22 @@ import nwhip  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--rows", type=int, default=131072)
-ap.add_argument("--sub", default="1,2,4")
+ap.add_argument("--shapes", default="4:1,2:1,1:1,2:2,1:2,1:4")
 ap.add_argument("--flags", type=int, default=0)
 ap.add_argument("--tag", default="")
 args = ap.parse_args()
 ctx = nwhip.Context(0)
 n2 = args.rows
 s2 = torch.from_numpy(nwhip.synth(2, n2)).cuda()
-for c in [int(x) for x in args.sub.split(",")]:
-    n1 = 64 * c - 1
+for c, nc in [tuple(int(v) for v in x.split(":")) for x in args.shapes.split(",")]:
+    n1 = 64 * c * nc  # one strip: columns 1 .. n1 (column 0 is the boundary)
     s1 = torch.from_numpy(nwhip.synth(1, n1)).cuda()
     tab = nwhip.Context.alloc_table(n1, n2)
-    ctx.fill(s1, s2, tab, substrips=c, flags=args.flags)
-    ms = min(ctx.fill(s1, s2, tab, substrips=c, flags=args.flags).kernel_ms for _ in range(3))
+    kw = dict(substrips=c, strip_waves=nc, flags=args.flags)
+    ctx.fill(s1, s2, tab, **kw)
+    ms = min(ctx.fill(s1, s2, tab, **kw).kernel_ms for _ in range(3))
     ns = ms * 1e6 / n2
-    print(f"{args.tag} C={c} rows={n2} ms={ms:.3f} ns/row={ns:.2f} cyc/step={ns * 2.39:.1f} "
-          f"cyc/cell={ns * 2.39 / (64 * c):.3f}", flush=True)
+    print(f"{args.tag} C={c} NC={nc} rows={n2} ms={ms:.3f} ns/row={ns:.2f} "
+          f"cyc/step={ns * 2.39:.1f} cyc/cell-per-wave={ns * 2.39 / (64 * c):.3f} "
+          f"cells/ns={64 * c * nc / ns:.2f}", flush=True)
     del tab

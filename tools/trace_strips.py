@@ -15,6 +15,7 @@ ap.add_argument("--n", type=int, default=32768)
 ap.add_argument("--waves", default="0")
 ap.add_argument("--flags", type=int, default=0)
 ap.add_argument("--sub", type=int, default=0)
+ap.add_argument("--nc", type=int, default=0)
 ap.add_argument("--save", default="")
 args = ap.parse_args()
 ctx = nwhip.Context(0)
@@ -26,9 +27,9 @@ nstrips = (n + 1 + 63) // 64
 tr = torch.zeros(nstrips * 16, dtype=torch.int64, device="cuda")
 for w in [int(x) for x in args.waves.split(",")]:
     ctx.set_trace(None)
-    r0 = ctx.fill(s1, s2, tab, waves=w, flags=args.flags, substrips=args.sub)
+    r0 = ctx.fill(s1, s2, tab, waves=w, flags=args.flags, substrips=args.sub, strip_waves=args.nc)
     ctx.set_trace(tr)
-    r = ctx.fill(s1, s2, tab, waves=w, flags=args.flags, substrips=args.sub)
+    r = ctx.fill(s1, s2, tab, waves=w, flags=args.flags, substrips=args.sub, strip_waves=args.nc)
     nstrips = r.strips
     ctx.set_trace(None)
     t = tr[: nstrips * 16].view(nstrips, 16).cpu().numpy().astype(np.float64)
@@ -65,7 +66,7 @@ for w in [int(x) for x in args.waves.split(",")]:
     busy = (dur - t[:, 3] / 100.0).sum()
     print(f"  sum(strip time - wait) / (waves * span) = {busy / (r.waves * en.max()):.3f}; "
           f"sum(wait) / (waves*span) = {t[:, 3].sum() / 100.0 / (r.waves * en.max()):.3f}")
-    print(f"n={n} K={r.substrips} waves={r.waves} strips={r.strips} kernel_ms={r.kernel_ms:.3f} (untraced {r0.kernel_ms:.3f}) "
+    print(f"n={n} C={r.substrips} NC={r.strip_waves} waves={r.waves} strips={r.strips} kernel_ms={r.kernel_ms:.3f} (untraced {r0.kernel_ms:.3f}) "
           f"span_us={en.max():.0f}")
     clk = (t[:, 7] - t[:, 6]) / np.maximum(t[:, 1] - t[:, 0], 1) * 100e6 / 1e9
     print(f"  effective shader clock GHz per strip: strip0 {clk[0]:.3f} p10 {np.percentile(clk, 10):.3f} "
@@ -77,5 +78,8 @@ for w in [int(x) for x in args.waves.split(",")]:
     print(f"  start lag us: med {np.median(lag):.2f} p10 {np.percentile(lag,10):.2f} p90 {np.percentile(lag,90):.2f}")
     print(f"  slow waits/strip: med {np.median(t[:,2]):.0f} max {t[:,2].max():.0f}; wait us/strip med "
           f"{np.median(t[:,3])/100:.0f} max {t[:,3].max()/100:.0f}")
+    print(f"  ring back-pressure us/strip: first wave med {np.median(t[:,11])/100:.0f} "
+          f"(strip0 {t[0,11]/100:.0f}); last wave med {np.median(t[:,12])/100:.0f} "
+          f"(strip0 {t[0,12]/100:.0f}); last wave feed wait med {np.median(t[:,13])/100:.0f}")
     for q in [0, 1, 2, nstrips // 4, nstrips // 2, nstrips - 2, nstrips - 1]:
         print(f"   strip {q}: start {st[q]:.1f} end {en[q]:.1f} dur {dur[q]:.1f} slow {t[q,2]:.0f} wait {t[q,3]/100:.1f}")
