@@ -68,8 +68,10 @@ struct Shape {
     int32_t K, NC;
 };
 
-constexpr int kDefaultSub = 2;         // columns per lane
-constexpr int kDefaultStripWaves = 2;  // chained compute waves per strip
+// default strip: 4 chained compute waves of 1 column per lane (256 columns); the
+// fastest shape at 256k (measured)
+constexpr int kDefaultSub = 1;         // columns per lane
+constexpr int kDefaultStripWaves = 4;  // chained compute waves per strip
 constexpr int kLdsPerCU = 160 * 1024;
 
 // col0: first swept column (1 when the table's column 1 starts a 256-byte line)

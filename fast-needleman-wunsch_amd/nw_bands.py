@@ -39,7 +39,7 @@ def plan(n2: int, nbands: int):
     return [nwhip.band_layout(n2, nbands, r) for r in range(nbands)]
 
 
-def resident_waves(device: int = 0, substrips: int = 2, strip_waves: int = 2) -> int:
+def resident_waves(device: int = 0, substrips: int = 0, strip_waves: int = 0) -> int:
     """Persistent strip workgroups that fit on the device at once (LDS-bound:
     nw_strip_lds_bytes per workgroup, 160 KiB per CU)."""
     import torch
@@ -53,8 +53,8 @@ class LocalBands:
     Each band gets at most 1/P of the resident workers so that all bands are
     co-resident (a band waiting for its halo never blocks its producer)."""
 
-    def __init__(self, n1: int, n2: int, nbands: int, device: int = 0, substrips: int = 2,
-                 strip_waves: int = 2):
+    def __init__(self, n1: int, n2: int, nbands: int, device: int = 0, substrips: int = 0,
+                 strip_waves: int = 0):
         import torch
         self.n1, self.n2, self.P, self.device = n1, n2, nbands, device
         self.substrips = substrips
