@@ -68,10 +68,10 @@ struct Shape {
     int32_t K, NC;
 };
 
-// default strip: 4 chained compute waves of 1 column per lane (256 columns); the
+// default strip: 2 chained compute waves of 2 columns per lane (256 columns); the
 // fastest shape at 256k (measured)
-constexpr int kDefaultSub = 1;         // columns per lane
-constexpr int kDefaultStripWaves = 4;  // chained compute waves per strip
+constexpr int kDefaultSub = 2;         // columns per lane
+constexpr int kDefaultStripWaves = 2;  // chained compute waves per strip
 constexpr int kLdsPerCU = 160 * 1024;
 
 // col0: first swept column (1 when the table's column 1 starts a 256-byte line)
@@ -212,6 +212,12 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
     if (!c || !d_t || n1 < 0 || n2 < 0 || n1 >= INT32_MAX || n2 >= INT32_MAX) return NW_ERR_ARG;
     if ((n1 > 0 && !d_s1) || (n2 > 0 && !d_s2)) return NW_ERR_ARG;
     if (!valid_params(p)) return NW_ERR_ARG;
+    // The kernel holds w = t - GAP*(i+j) in int32 next to a "minus infinity" of
+    // -2^29: |w| <= (max|score| + |GAP|) * (i + j) must stay below 2^28.
+    {
+        const long long m = std::max({std::llabs(p->match), std::llabs(p->mismatch), std::llabs(p->gap)});
+        if ((m + std::llabs(p->gap)) * (long long)(n1 + n2 + 2) >= (1LL << 28)) return NW_ERR_ARG;
+    }
     // any 64-multiple pitch that holds nCols = n1 + 1 (nw_table_pitch adds the
     // slack that lets the strips start at column 1)
     if (pitch < n1 + 1 || pitch % nw::kWave != 0) return NW_ERR_ARG;
@@ -257,10 +263,10 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
     NW_HIP_TRY(hipMemsetAsync(c->ctrl, 0, 32, (hipStream_t)stream));
     const uint8_t *s1u = n1 > 0 ? (const uint8_t *)d_s1 : (const uint8_t *)c->ctrl;
     const uint8_t *s2u = n2 > 0 ? (const uint8_t *)d_s2 : (const uint8_t *)c->ctrl;
-    // v_perm score tables when every substitution score minus GAP fits int8
+    // v_perm score tables when every substitution score minus 2*GAP fits int8
     // (the kernel falls back to compares on the device when s1 holds more than
     // kMaxPerm distinct characters).
-    const bool perm_ok = fits_i8(p->match - p->gap) && fits_i8(p->mismatch - p->gap) &&
+    const bool perm_ok = fits_i8(p->match - 2 * p->gap) && fits_i8(p->mismatch - 2 * p->gap) &&
                          !(p->flags & NW_FLAG_NO_PROFILE);
     if (nw::launch_rowpack(s1u, n1, s2u, n2, 0, perm_ok ? 1 : 0, c->meta, c->rowpack, qlen,
                            stream) != hipSuccess)

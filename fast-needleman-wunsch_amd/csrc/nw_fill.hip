@@ -19,15 +19,15 @@
 //         Lane l owns the C consecutive columns j*64C + C*l + k and at step s
 //         computes row i = s - l for all of them -- an anti-diagonal wavefront
 //         across the lanes, a left-to-right chain of C cells inside each lane.
-//         Per cell:
-//           d = diag' + s'(a, b)      v_add_u32_sdwa (a byte of a v_perm result)
-//           t = max3(d, up', left')   v_max3_i32
-//           u = t + GAP               v_add_u32   (u = what neighbours consume)
-//         s'(a, b) = s(a, b) - GAP comes from a per-lane 8-byte score table
+//         Cells are held as w = t - GAP*(i+j), in which both gap terms vanish
+//         (the store waves add GAP*(i+j) back):
+//           d = w_diag + s'(a, b)     v_add_u32_sdwa (a byte of a v_perm result)
+//           w = max3(d, w_up, w_left) v_max3_i32
+//         s'(a, b) = s(a, b) - 2*GAP comes from a per-lane 8-byte score table
 //         indexed by the (mapped) row character: ONE v_perm_b32 gives column
-//         k's scores for four consecutive steps.  up' is the lane's own
-//         register; left'/diag' of column k > 0 are the lane's own column k-1.
-//         Column 0 of the wave takes left' from lane l-1's column C-1 (DPP
+//         k's scores for four consecutive steps.  w_up is the lane's own
+//         register; w_left/w_diag of column k > 0 are the lane's own column k-1.
+//         Column 0 of the wave takes w_left from lane l-1's column C-1 (DPP
 //         wave_shr:1, whose "old" operand feeds lane 0 from the FEED: a ring of
 //         the left neighbour's right column in LDS).  Each step's C results go
 //         to the wave's LDS ring indexed by ANTI-DIAGONAL (128 slots; slot =
@@ -248,17 +248,17 @@ __device__ __forceinline__ void static_for(F &&f) {
 //   SUB_PERM : the row words hold MAPPED row characters (index 0..7 of the
 //              character among s1's distinct ones, 7 = "in no column"); each
 //              lane keeps, per column k, the 8-byte table
-//              T_k[x] = s(a_k, char x) - GAP (int8).  v_perm_b32(T_k, word)
+//              T_k[x] = s(a_k, char x) - 2*GAP (int8).  v_perm_b32(T_k, word)
 //              yields column k's scores for the 4 rows of a row word (one
-//              byte per step), so per cell d = diag' + sext(byte): ONE
+//              byte per step), so per cell d = w_diag + sext(byte): ONE
 //              v_add_u32_sdwa, no compare.  Needs <= 7 distinct column
-//              characters and both scores - GAP in int8.
-//   SUB_UNIT : match - mismatch == 1: d = diag' + mm' + [a == b]
+//              characters and both scores - 2*GAP in int8.
+//   SUB_UNIT : match - mismatch == 1: d = w_diag + mm' + [a == b]
 //              (v_cmp_eq_u32_sdwa -> vcc -> v_addc) on raw characters
-//   SUB_GEN  : d = diag' + (a == b ? ms' : mm')  (v_cmp -> vcc -> v_cndmask, add)
+//   SUB_GEN  : d = w_diag + (a == b ? ms' : mm')  (v_cmp -> vcc -> v_cndmask, add)
 // The compare forms test raw byte equality, the reference's match test
-// (serial.cpp:23-24); ms' / mm' / the table bytes have GAP pre-subtracted
-// because diag' = t + GAP.
+// (serial.cpp:23-24); ms' / mm' / the table bytes have 2*GAP pre-subtracted
+// because the cells hold w = t - GAP*(i+j).
 enum Sub { SUB_PERM = 0, SUB_UNIT = 1, SUB_GEN = 2 };
 
 template <int QB, int KB, int MODE>
@@ -294,8 +294,8 @@ __device__ __forceinline__ int32_t diag_plus_sub(uint32_t w, uint32_t apk, int32
 // Per-lane state of a compute wave on one strip.
 template <int C>
 struct Lanes {
-    int32_t u[C];      // t + GAP of the lane's current row, column k
-    int32_t dg;        // diag' of column 0 for the next step (= last step's left')
+    int32_t u[C];      // w = t - GAP*(i+j) of the lane's current row, column k
+    int32_t dg;        // w_diag of column 0 for the next step (= last step's w_left)
     int32_t rr;        // RAMP: row of this lane at the current step
     uint32_t apk;      // raw column characters of the lane, byte k = column k
     uint32_t tlo[C];   // SUB_PERM score tables: bytes 0..3 / 4..7 of T_k
@@ -309,7 +309,7 @@ struct Lanes {
 // Where a compute wave's feed comes from.
 enum FeedSrc { FEED_BOUNDARY = 0, FEED_GRAN = 1, FEED_LDS = 2 };
 
-// The feed of one iteration: the left neighbour's right column (+ GAP) for rows
+// The feed of one iteration: the left neighbour's right column (w form) for rows
 // 64*it .. 64*it+63, in this wave's LDS feed ring.  `ready` leading 16-row
 // chunks were found there when the iteration started; before the group that
 // first reads chunk c >= ready, run_iter waits for it: FEED_GRAN polls the
@@ -376,7 +376,7 @@ __device__ __forceinline__ void run_iter(char *__restrict__ lds, int it, const u
     auto publish = [&](int c) {
         if (b < 0) return;
         if (O.lds) {
-            if (lane < 16) O.ring[(64 * b + 16 * c + lane) & (kFeedRows - 1)] = S.rcol + O.gap;
+            if (lane < 16) O.ring[(64 * b + 16 * c + lane) & (kFeedRows - 1)] = S.rcol;
             lds_order();
             ctr_store(O.pub, 64 * b + 16 * c + 16);
         } else if (lane < 16) {
@@ -407,7 +407,7 @@ __device__ __forceinline__ void run_iter(char *__restrict__ lds, int it, const u
                 if (F.src == FEED_GRAN) {
                     const uint64_t v = wait_chunk(F.g, F.tag, c, ctrl, 2);
                     F.dead |= !__all((lane >> 4) != c || (uint32_t)(v >> 32) == F.tag);
-                    if ((lane >> 4) == c) F.ring[((it & 3) << 6) + lane] = (int32_t)(uint32_t)v + F.gap;
+                    if ((lane >> 4) == c) F.ring[((it & 3) << 6) + lane] = (int32_t)(uint32_t)v;
                 } else {
                     F.dead |= wait_counter(F.pub, s0 + 16 * (c + 1), ctrl, 3) == kDead;
                     lds_order();  // feed reads after the counter that published them
@@ -444,18 +444,14 @@ __device__ __forceinline__ void run_iter(char *__restrict__ lds, int it, const u
                 constexpr int k = decltype(kc)::value;
                 const uint32_t w = MODE == SUB_PERM ? sc[k] : word;
                 const int32_t d = diag_plus_sub<q, k, MODE>(w, S.apk, diag, msp, mmp);
-                int32_t t = max(max(d, S.u[k]), left);  // max(diag+s, up+GAP, left+GAP)
+                // w = max(w_diag + s - 2 GAP, w_up, w_left)  (w = t - GAP*(i+j))
+                int32_t x = max(max(d, S.u[k]), left);
                 diag = S.u[k];
-                if constexpr (RAMP) {
-                    // lanes still above row 1 hold row 0 (the top boundary / halo)
-                    const int32_t un = act ? t + gap : S.u[k];
-                    t = un - gap;
-                    S.u[k] = un;
-                } else {
-                    S.u[k] = t + gap;
-                }
-                left = S.u[k];
-                set_comp<C>(tv, k, t);
+                // lanes still above row 1 hold row 0 (the top boundary / halo)
+                if constexpr (RAMP) x = act ? x : S.u[k];
+                S.u[k] = x;
+                left = x;
+                set_comp<C>(tv, k, x);
             });
             *(VT *)(ringw + u * L::kSlot) = tv;  // ring slot 64*HALF + u
             // right column of block b, chunk c = u / 16: read back after the
@@ -487,7 +483,7 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
                                               int j, int lane) {
     typedef Lay<C, NC> L;
     const int32_t gap = A.gap;
-    const int32_t msp = A.match - gap, mmp = A.mismatch - gap;
+    const int32_t msp = A.match - 2 * gap, mmp = A.mismatch - 2 * gap;
     const int64_t c0 = A.col0 + (int64_t)p * (NC * 64 * C) + (int64_t)j * (64 * C);
     const int64_t cl = c0 + (int64_t)C * lane;  // first column of this lane
     int32_t *ctr = (int32_t *)(lds + L::kCtl) + j * L::kCtlWords;
@@ -532,7 +528,7 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
     if (j == 0) ((int32_t *)(lds + L::kCtl))[L::kStripWord + 1] = bnd0;
     Lanes<C> S;
     S.apk = 0;
-    // SUB_PERM tables: T_k[x] = s(a_k, chars[x]) - GAP for x < 8 (x = 7 and any
+    // SUB_PERM tables: T_k[x] = s(a_k, chars[x]) - 2*GAP for x < 8 (x = 7 and any
     // x >= nprof: a row character in no column, always a mismatch)
     const uint32_t mmb = ((uint32_t)mmp & 255u) * 0x01010101u;
 #pragma unroll
@@ -540,7 +536,7 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
         const int64_t c = cl + k;
         const uint32_t a = (c >= 1 && c <= A.n1) ? (uint32_t)A.s1[c - 1] : 0u;
         S.apk |= a << (8 * k);
-        S.u[k] = top[k] + gap;  // t[0][c] + GAP
+        S.u[k] = top[k] - (int32_t)((cl + k) * (int64_t)gap);  // w[0][c] = t[0][c] - GAP*c
         if constexpr (MODE == SUB_PERM) {
             const uint32_t x = (c >= 1 && c <= A.n1) ? (uint32_t)A.charmap[a] : 0xFFu;
             const uint32_t msb = (uint32_t)msp & 255u;
@@ -648,7 +644,7 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
                     F.wticks += __builtin_amdgcn_s_memrealtime() - w0;
                     F.ready = max(1, chunks_ready(gv, F.tag));
                 }
-                F.ring[((it & 3) << 6) + lane] = (int32_t)(uint32_t)gv + gap;
+                F.ring[((it & 3) << 6) + lane] = (int32_t)(uint32_t)gv;
             } else if (F.src == FEED_LDS) {
                 int32_t pv = __builtin_amdgcn_readfirstlane(ctr_load(F.pub));
                 if (pv < it * 64 + 16) {
@@ -663,10 +659,10 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
                 lds_order();  // feed reads after the counter that published them
             } else {
                 // strip 0, wave 0: left of column col0 is the boundary column:
-                // t[r][0] + GAP with col0 = 1, "minus infinity" when col0 = 0 (the
-                // lane holding column 0 then computes t[r][0] = t[r-1][0] + GAP)
-                const int32_t r = it * 64 + lane;
-                F.ring[((it & 3) << 6) + lane] = A.col0 ? bnd0 + (r + 1) * gap : kNeg;
+                // w[r][0] = t[r][0] - GAP*r = t[0][0] with col0 = 1, "minus infinity"
+                // when col0 = 0 (the lane holding column 0 then computes
+                // w[r][0] = w[r-1][0], i.e. t[r][0] = t[r-1][0] + GAP)
+                F.ring[((it & 3) << 6) + lane] = A.col0 ? bnd0 : kNeg;
             }
             if (traced) tsee = __builtin_amdgcn_s_memrealtime();
         } else if (F.src != FEED_LDS) {
@@ -757,6 +753,12 @@ __device__ __forceinline__ void store_strip(const FillArgs &A, char *__restrict_
     const int64_t rowb = timing ? 0 : A.pitch * 4;
     char *scr = (char *)(A.scratch + (int64_t)blockIdx.x * kScratchWords);
     const int32_t f0 = q * BATCH;
+    // the ring holds w = t - GAP*(r + c) (run_iter): kc[e] = GAP*(r + c) of element
+    // e of this lane's piece in its current batch (wrapping int32, like the cells)
+    const uint32_t ug = (uint32_t)A.gap;
+    uint32_t kc[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) kc[e] = ug * (uint32_t)(f0 + ro) + ug * (uint32_t)(c0 + 4 * cq + e);
     char *rowp = timing ? scr : (char *)(A.table + c0) + (int64_t)f0 * rowb;
     const uint32_t voff = (uint32_t)(ro * rowb) + (uint32_t)cq * 16u;
     // col0 = 1: strip 0's first ring also stores the boundary column 0,
@@ -791,11 +793,14 @@ __device__ __forceinline__ void store_strip(const FillArgs &A, char *__restrict_
                 const VT x = *(const VT *)(ring + pa[m]);
                 pa[m] = adv(pa[m], NR);
 #pragma unroll
-                for (int k = 0; k < C; ++k) v[g][m * C + k] = (uint32_t)comp<C>(x, k);
+                for (int k = 0; k < C; ++k)
+                    v[g][m * C + k] = (uint32_t)comp<C>(x, k) + kc[m * C + k] + ug * (uint32_t)(g * NR);
             }
         }
 #pragma unroll
         for (int m = 0; m < NR; ++m) pa[m] = adv(pa[m], (NS - 1) * BATCH);  // skip the others'
+#pragma unroll
+        for (int e = 0; e < 4; ++e) kc[e] += ug * (uint32_t)(NS * BATCH);
         if (want - f == BATCH) {
 #pragma unroll
             for (int g = 0; g < NG; ++g)
@@ -1004,6 +1009,6 @@ int lds_bytes(int substrips, int strip_waves) {
     }
 }
 
-const char *kernel_variant() { return "strip-NCx64xC-chained-computewaves+storewaves-diagring128-vperm-gran16"; }
+const char *kernel_variant() { return "strip-NCx64xC-chained-computewaves+storewaves-diagring128-vperm-gran16-wform"; }
 
 }  // namespace nw

@@ -214,13 +214,13 @@ def table_offset() -> int:
 
 def strip_shape(substrips: int = 0, strip_waves: int = 0) -> tuple[int, int]:
     """(C, NC) the library uses for these nw_params values (0 = auto), as
-    make_shape in nw_capi.cpp: auto = (1, 4); C alone implies 256-column strips."""
-    c = substrips if substrips > 0 else 1
+    make_shape in nw_capi.cpp: auto = (2, 2); C alone implies 256-column strips."""
+    c = substrips if substrips > 0 else 2
     if strip_waves > 0:
         return c, strip_waves
     if substrips > 0:
         return c, {1: 4, 2: 2, 4: 1}[c]
-    return c, 4
+    return c, 2
 
 
 def strip_lds_bytes(substrips: int, strip_waves: int) -> int:

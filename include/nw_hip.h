@@ -63,7 +63,7 @@ typedef struct nw_params {
     int32_t substrips; /* columns per lane C of a compute wave (1, 2 or 4); 0 = auto */
     int32_t strip_waves; /* chained compute waves per strip NC (1, 2 or 4); 0 = auto.
                             A strip is NC * 64 * C columns; supported (C, NC):
-                            (4,1) (2,1) (1,1) (2,2) (1,2) (1,4); auto = (1,4) */
+                            (4,1) (2,1) (1,1) (2,2) (1,2) (1,4); auto = (2,2) */
 } nw_params;
 
 typedef struct nw_result {

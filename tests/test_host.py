@@ -67,7 +67,7 @@ def test_strip_shapes_lds():
         b = nwhip.strip_lds_bytes(c, nc)
         assert 0 < b <= 160 * 1024, (c, nc, b)
     assert nwhip.strip_lds_bytes(4, 2) == -1 and nwhip.strip_lds_bytes(3, 1) == -1
-    assert nwhip.strip_shape() == (1, 4)
+    assert nwhip.strip_shape() == (2, 2)
     assert nwhip.strip_shape(4) == (4, 1) and nwhip.strip_shape(1) == (1, 4)
     assert nwhip.strip_shape(2, 1) == (2, 1)
 
