@@ -177,6 +177,18 @@ def test_other_schemes_vs_oracle(scheme):
     np.testing.assert_array_equal(t, oracle.fill(s1, s2, scheme))
 
 
+def test_score_range_refused():
+    """The kernel holds w = t - GAP*(i+j) in int32: a scheme/size whose
+    (max|score| + |GAP|) * (n1 + n2 + 2) reaches 2^28 is refused (NW_ERR_ARG),
+    never silently wrapped; just below the bound it fills."""
+    s = nwhip.synth(1, 16400)
+    with pytest.raises(nwhip.NwError) as e:
+        nwhip.score(s, s, (4095, -4095, -4095))
+    assert e.value.status == nwhip.NW_ERR_ARG
+    small = s[:1000]
+    assert nwhip.score(small, small, (4095, -4095, -4095)) == oracle.score(small, small, (4095, -4095, -4095))
+
+
 @pytest.mark.parametrize("waves", [1, 2, 3, 5, 8, 17, 64])
 @pytest.mark.parametrize("strip", STRIP_SHAPES)
 def test_worker_count_independent(torch, ctx, waves, strip):
