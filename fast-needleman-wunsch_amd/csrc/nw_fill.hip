@@ -166,7 +166,15 @@ __device__ __forceinline__ void ctr_store(int32_t *p, int32_t v) {
 // Bounded: gives up -- raising the error word -- after kTimeoutTicks, or at once
 // if another wave already raised it.  Returns the last value read; the caller
 // re-checks its tag.
-__device__ __forceinline__ uint64_t wait_chunk(const uint64_t *g, uint32_t tag, int c,
+//
+// Every loop that polls global memory lives in a __noinline__ function reached
+// only on a slow path.  Inlined, such a loop issues an unknown number of vector
+// memory operations, after which the compiler can no longer count the prefetch
+// loads still in flight and waits for ALL of them (s_waitcnt vmcnt(0)) before
+// the next use of any -- once per iteration, on the fast path too.  A call
+// drains the counters on the slow path only (the callee's entry waits), so the
+// fast path keeps counted vmcnt(N) waits.
+__device__ __noinline__ uint64_t wait_chunk(const uint64_t *g, uint32_t tag, int c,
                                             uint32_t *ctrl, uint32_t site) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     const int lane = threadIdx.x & 63;
@@ -194,9 +202,10 @@ __device__ __forceinline__ int chunks_ready(uint64_t v, uint32_t tag) {
 }
 
 // Bounded spin until the LDS counter *p reaches `need`; returns the value seen
-// (kDead once the error word is raised or the watchdog expires).
-__device__ __forceinline__ int32_t wait_counter(const int32_t *p, int32_t need, uint32_t *ctrl,
-                                             uint32_t site) {
+// (kDead once the error word is raised or the watchdog expires).  Slow path of
+// wait_counter (out of line: see wait_chunk).
+__device__ __noinline__ int32_t wait_counter_slow(const int32_t *p, int32_t need, uint32_t *ctrl,
+                                                  uint32_t site) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
         const int32_t v = __builtin_amdgcn_readfirstlane(ctr_load(p));
@@ -208,6 +217,12 @@ __device__ __forceinline__ int32_t wait_counter(const int32_t *p, int32_t need, 
         }
         __builtin_amdgcn_s_sleep(1);
     }
+}
+__device__ __forceinline__ int32_t wait_counter(const int32_t *p, int32_t need, uint32_t *ctrl,
+                                             uint32_t site) {
+    const int32_t v = __builtin_amdgcn_readfirstlane(ctr_load(p));
+    if (v >= need) return v;
+    return __builtin_amdgcn_readfirstlane(wait_counter_slow(p, need, ctrl, site));
 }
 
 // Rows every store wave of a ring has read out of it (each publishes the
@@ -611,6 +626,7 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
     const uint64_t cstart = __builtin_amdgcn_s_memtime();
     uint64_t tq1 = 0, tmid = 0;  // trace: times iterations nblocks/4 and nblocks/2 started
     uint64_t tsee = 0, twait = 0;  // trace: see / wait start, block nblocks/2 chunk 0
+    uint64_t tin = 0;              // trace: shader cycles spent inside run_iter
 
     // Iteration it: feed for block it (consumes buffer it % NB), prefetch for
     // it+PD, 64 steps, block it-1's right column published.  A watchdog trip
@@ -673,8 +689,10 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
         load_packs(pkp, it + PD, lane, pkb[ISS]);
         const int b = it - 1;  // block whose right column this iteration publishes
         uint64_t *gp = (b >= 0 && b < nblocks) ? gout + (int64_t)b * 64 + lane : gscr;
+        const uint64_t ti0 = A.trace != nullptr ? __builtin_amdgcn_s_memtime() : 0;
         run_iter<C, NC, MODE, RAMP, HALF>(lds, it, pkb[CONS], msp, mmp, gap, S, ctr, rd, b, gp, tagw,
                                           O, A.ctrl, F, lane);
+        if (A.trace != nullptr) tin += __builtin_amdgcn_s_memtime() - ti0;
         ctr_store(ctr + 2, it + 1);  // iterations done (feed-ring space for wave j-1)
         dead = F.dead;
     };
@@ -708,6 +726,7 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
             tr[9] = tsee;
             tr[10] = twait;
             tr[11] = F.rticks;
+            tr[14] = tin;
         }
         if (j == NC - 1) {
             tr[1] = __builtin_amdgcn_s_memrealtime();
@@ -715,6 +734,7 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
             tr[8] = F.tpub;
             tr[12] = F.rticks;
             tr[13] = F.wticks;
+            tr[15] = tin;
         }
     }
 }
@@ -775,6 +795,10 @@ __device__ __forceinline__ void store_strip(const FillArgs &A, char *__restrict_
     // `rows` further down the ring (the piece offset a * 4C < kSlot survives the mask)
     auto adv = [&](uint32_t x, uint32_t rows) { return (x + rows * L::kSlot) & kMask; };
     int32_t *mine = ctr + 3 + q;
+    if (A.flags & 8) {  // debug: no store waves at all (compute-pace probe, timing only)
+        ctr_store(mine, kDone);
+        return;
+    }
     int32_t avail = 0;  // rows complete in the ring (steps written - 63)
     for (int32_t f = f0; f < nrows; f += NS * BATCH) {
         const int32_t want = min(f + BATCH, nrows);
@@ -784,6 +808,12 @@ __device__ __forceinline__ void store_strip(const FillArgs &A, char *__restrict_
             avail = (sa == kDone || sa == kDead) ? nrows : min(sa - 63, nrows);
             lds_order();  // ring reads after the counter that released them
             if (bcol) bnd0 = *bnd0p;
+        }
+        if (A.flags & 4) {  // debug: drain the ring without reading it (compute-pace probe)
+            rowp += NS * BATCH * rowb;
+            lds_order();
+            ctr_store(mine, f + NS * BATCH);
+            continue;
         }
         u32x4 v[NG];
 #pragma unroll
@@ -974,7 +1004,18 @@ static void launch_c(const FillArgs &a, int grid, hipStream_t s) {
 }
 
 // Supported (columns per lane, compute waves per strip) shapes.
+// Experiment builds (make variant DEFS="-DNW_ONLY_C=2 -DNW_ONLY_NC=2") instantiate
+// one strip shape only, which cuts the compile from minutes to seconds.
+#ifdef NW_ONLY_C
+#define NW_SHAPE(c, nc) ((c) == NW_ONLY_C && (nc) == NW_ONLY_NC)
+#else
+#define NW_SHAPE(c, nc) true
+#endif
+
 bool shape_ok(int substrips, int strip_waves) {
+#ifdef NW_ONLY_C
+    if (substrips != NW_ONLY_C || strip_waves != NW_ONLY_NC) return false;
+#endif
     switch (substrips * 8 + strip_waves) {
         case 4 * 8 + 1: case 2 * 8 + 1: case 1 * 8 + 1:
         case 2 * 8 + 2: case 1 * 8 + 2: case 1 * 8 + 4:
@@ -986,13 +1027,12 @@ bool shape_ok(int substrips, int strip_waves) {
 
 int launch_fill(const FillArgs &a, int substrips, int strip_waves, int grid, void *stream) {
     hipStream_t s = (hipStream_t)stream;
+    if (!shape_ok(substrips, strip_waves)) return (int)hipErrorInvalidValue;
     switch (substrips * 8 + strip_waves) {
-        case 4 * 8 + 1: launch_c<4, 1>(a, grid, s); break;
-        case 2 * 8 + 1: launch_c<2, 1>(a, grid, s); break;
-        case 1 * 8 + 1: launch_c<1, 1>(a, grid, s); break;
-        case 2 * 8 + 2: launch_c<2, 2>(a, grid, s); break;
-        case 1 * 8 + 2: launch_c<1, 2>(a, grid, s); break;
-        case 1 * 8 + 4: launch_c<1, 4>(a, grid, s); break;
+#define NW_CASE(c, nc) \
+        case c * 8 + nc: if constexpr (NW_SHAPE(c, nc)) launch_c<c, nc>(a, grid, s); break;
+        NW_CASE(4, 1) NW_CASE(2, 1) NW_CASE(1, 1) NW_CASE(2, 2) NW_CASE(1, 2) NW_CASE(1, 4)
+#undef NW_CASE
         default: return (int)hipErrorInvalidValue;
     }
     return (int)hipGetLastError();

@@ -81,5 +81,8 @@ for w in [int(x) for x in args.waves.split(",")]:
     print(f"  ring back-pressure us/strip: first wave med {np.median(t[:,11])/100:.0f} "
           f"(strip0 {t[0,11]/100:.0f}); last wave med {np.median(t[:,12])/100:.0f} "
           f"(strip0 {t[0,12]/100:.0f}); last wave feed wait med {np.median(t[:,13])/100:.0f}")
+    cyc = (t[:, 7] - t[:, 6])
+    print(f"  cycles/step inside run_iter: first wave strip0 {t[0,14]/n:.1f} med {np.median(t[:,14])/n:.1f}; "
+          f"last wave strip0 {t[0,15]/n:.1f} med {np.median(t[:,15])/n:.1f}; whole strip med {np.median(cyc)/n:.1f}")
     for q in [0, 1, 2, nstrips // 4, nstrips // 2, nstrips - 2, nstrips - 1]:
         print(f"   strip {q}: start {st[q]:.1f} end {en[q]:.1f} dur {dur[q]:.1f} slow {t[q,2]:.0f} wait {t[q,3]/100:.1f}")
