@@ -16,6 +16,7 @@
 
 #include "nw_hip.h"
 #include "nw_internal.h"
+#include "nw_tuned.h"
 
 struct nw_ctx {
     int device = 0;
@@ -51,15 +52,17 @@ inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
         }                                                                        \
     } while (0)
 
-int grow(void **p, size_t *cap, size_t need, bool zero) {
+// (Re)allocate a workspace buffer; returns NW_OK and sets *fresh when it is new.
+int grow(void **p, size_t *cap, size_t need, bool *fresh = nullptr) {
+    if (fresh) *fresh = false;
     if (need <= *cap) return NW_OK;
     if (*p) (void)hipFree(*p);
     *p = nullptr;
     *cap = 0;
     need = (size_t)round_up((int64_t)need, 1 << 21);
     NW_HIP_TRY(hipMalloc(p, need));
-    if (zero) NW_HIP_TRY(hipMemset(*p, 0, need));
     *cap = need;
+    if (fresh) *fresh = true;
     return NW_OK;
 }
 
@@ -68,18 +71,31 @@ struct Shape {
     int32_t K, NC;
 };
 
-// default strip: 2 chained compute waves of 2 columns per lane (256 columns); the
-// fastest shape at 256k (measured)
-constexpr int kDefaultSub = 2;         // columns per lane
-constexpr int kDefaultStripWaves = 2;  // chained compute waves per strip
 constexpr int kLdsPerCU = 160 * 1024;
+
+// Strip shape for nw_params.substrips = strip_waves = 0: the measured table of
+// tools/tune.py (csrc/nw_tuned.h, by table size), else (2, 2).
+void tuned_shape(int64_t n1, int64_t n2, int32_t *c, int32_t *nc) {
+    const double cells = (double)(n1 + 1) * (double)(n2 + 1);
+    *c = 2;
+    *nc = 2;
+    for (const auto &e : nw::kTuned)
+        if (cells >= e.min_cells && nw::shape_ok(e.c, e.nc)) {
+            *c = e.c;
+            *nc = e.nc;
+        }
+}
 
 // col0: first swept column (1 when the table's column 1 starts a 256-byte line)
 Shape make_shape(int64_t n1, int64_t n2, int32_t waves_req, int32_t sub_req, int32_t nc_req,
                  int cus, int64_t col0) {
     Shape s;
-    s.K = sub_req > 0 ? sub_req : kDefaultSub;
-    s.NC = nc_req > 0 ? nc_req : (sub_req > 0 ? (s.K == 1 ? 4 : s.K == 2 ? 2 : 1) : kDefaultStripWaves);
+    if (sub_req <= 0 && nc_req <= 0) {
+        tuned_shape(n1, n2, &s.K, &s.NC);
+    } else {
+        s.K = sub_req > 0 ? sub_req : 2;
+        s.NC = nc_req > 0 ? nc_req : (s.K == 1 ? 4 : s.K == 2 ? 2 : 1);
+    }
     s.nRows = n2 + 1;
     s.nCols = n1 + 1;
     const int64_t width = (int64_t)nw::kWave * s.K * s.NC;
@@ -104,6 +120,7 @@ bool valid_params(const nw_params *p) {
     if (p->substrips != 0 && p->substrips != 1 && p->substrips != 2 && p->substrips != 4) return false;
     if (p->strip_waves != 0 && p->strip_waves != 1 && p->strip_waves != 2 && p->strip_waves != 4)
         return false;
+    if (p->timeout_ms < 0) return false;
     // keep every intermediate far from int32 overflow (|score| < 2^29)
     const int32_t lim = 1 << 12;
     return std::abs(p->match) < lim && std::abs(p->mismatch) < lim && std::abs(p->gap) < lim;
@@ -213,10 +230,12 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
     if ((n1 > 0 && !d_s1) || (n2 > 0 && !d_s2)) return NW_ERR_ARG;
     if (!valid_params(p)) return NW_ERR_ARG;
     // The kernel holds w = t - GAP*(i+j) in int32 next to a "minus infinity" of
-    // -2^29: |w| <= (max|score| + |GAP|) * (i + j) must stay below 2^28.
+    // -2^29: |w| <= (max|score| + |GAP|) * (i + j) must stay below 2^28, with i the
+    // GLOBAL row (a band's halo row carries the values of row band->row0).
     {
         const long long m = std::max({std::llabs(p->match), std::llabs(p->mismatch), std::llabs(p->gap)});
-        if ((m + std::llabs(p->gap)) * (long long)(n1 + n2 + 2) >= (1LL << 28)) return NW_ERR_ARG;
+        const long long i_max = (long long)n2 + (band ? (long long)band->row0 : 0);
+        if ((m + std::llabs(p->gap)) * (long long)(n1 + i_max + 2) >= (1LL << 28)) return NW_ERR_ARG;
     }
     // any 64-multiple pitch that holds nCols = n1 + 1 (nw_table_pitch adds the
     // slack that lets the strips start at column 1)
@@ -244,9 +263,14 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
     int st;
     // Hand-off granules.  (Re)allocation zeroes them; tags are then unique per
     // (launch, strip) as long as tagbase does not wrap -- re-zero when it would.
+    // A new buffer is zeroed on the launch stream (ordered before the kernels
+    // below on any stream, also a non-blocking one): reused device memory may
+    // still hold granules whose tags match this context's fresh tagbase.
     const size_t gran_need = (size_t)(s.M * s.gstride) * sizeof(uint64_t);
-    if (gran_need > c->gran_cap) {
-        if ((st = grow((void **)&c->gran, &c->gran_cap, gran_need, true)) != NW_OK) return st;
+    bool fresh = false;
+    if ((st = grow((void **)&c->gran, &c->gran_cap, gran_need, &fresh)) != NW_OK) return st;
+    if (fresh) {
+        NW_HIP_TRY(hipMemsetAsync(c->gran, 0, c->gran_cap, (hipStream_t)stream));
         c->tagbase = 1;
     }
     if ((uint64_t)c->tagbase + (uint64_t)s.nstrips + 2u >= 0xFFFFFFF0ull) {
@@ -254,10 +278,8 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
         c->tagbase = 1;
     }
     const int64_t qlen = nw::rowpack_len((int32_t)s.nblocks);
-    if ((st = grow((void **)&c->rowpack, &c->rowpack_cap, (size_t)qlen * 16, false)) != NW_OK)
-        return st;
-    if ((st = grow((void **)&c->scratch, &c->scratch_cap,
-                   (size_t)s.waves * nw::kScratchWords * 4, false)) != NW_OK)
+    if ((st = grow((void **)&c->rowpack, &c->rowpack_cap, (size_t)qlen * 16)) != NW_OK) return st;
+    if ((st = grow((void **)&c->scratch, &c->scratch_cap, (size_t)s.waves * nw::kScratchWords * 4)) != NW_OK)
         return st;
 
     NW_HIP_TRY(hipMemsetAsync(c->ctrl, 0, 32, (hipStream_t)stream));
@@ -301,6 +323,8 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
     a.mismatch = p->mismatch;
     a.gap = p->gap;
     a.flags = p->flags;
+    // s_memrealtime runs at 100 MHz: 100000 ticks per ms
+    a.timeout_ticks = (uint64_t)(p->timeout_ms > 0 ? p->timeout_ms : 20000) * 100000ull;
     if (nw::launch_fill(a, s.K, s.NC, (int)s.waves, stream) != hipSuccess) return NW_ERR_HIP;
     c->tagbase += (uint32_t)s.nstrips + 1u;
     c->last_waves = (int)s.waves;
@@ -474,8 +498,8 @@ int nw_fill(const int8_t *s1, int64_t n1, const int8_t *s2, int64_t n2, const nw
     return st;
 }
 
-// Debug hook (not part of the public ABI): the control words of the last launch
-// (ticket, error code, watchdog site / need / seen -- nw_fill.hip give_up).
+// Debug hook: the control words of the last launch (ticket, error code, watchdog
+// site / need / seen -- nw_fill.hip give_up); include/nw_hip.h documents them.
 int nw_debug_ctrl(nw_ctx *c, uint32_t *out8) {
     if (!c || !out8) return NW_ERR_ARG;
     NW_HIP_TRY(hipSetDevice(c->device));
@@ -484,12 +508,21 @@ int nw_debug_ctrl(nw_ctx *c, uint32_t *out8) {
     return NW_OK;
 }
 
-// Debug hook (not part of the public ABI): per-strip trace buffer, device memory
-// of nstrips * 8 uint64 (see nwhip.Context.set_trace); NULL = off.
+// Debug hook: per-strip trace buffer, device memory of at least
+// strips * nw_debug_trace_words() uint64 (see nwhip.Context.set_trace); NULL = off.
 int nw_debug_set_trace(nw_ctx *c, void *d_trace) {
     if (!c) return NW_ERR_ARG;
     c->trace = (uint64_t *)d_trace;
     return NW_OK;
+}
+
+int32_t nw_debug_trace_words(void) { return nw::kTraceWords; }
+
+void nw_tuned_shape(int64_t n1, int64_t n2, int32_t *substrips, int32_t *strip_waves) {
+    int32_t c = 2, nc = 2;
+    if (n1 >= 0 && n2 >= 0) tuned_shape(n1, n2, &c, &nc);
+    if (substrips) *substrips = c;
+    if (strip_waves) *strip_waves = nc;
 }
 
 }  // extern "C"

@@ -63,7 +63,7 @@
 namespace nw {
 
 // s_memrealtime runs at 100 MHz on gfx9: 20 s watchdog for every bounded spin.
-constexpr uint64_t kTimeoutTicks = 100000000ull * 20ull;
+// (the bound of every spin: FillArgs::timeout_ticks, 20 s unless nw_params.timeout_ms says otherwise)
 constexpr int32_t kDone = 0x7FFFFFFF;  // counter value: "no more waiting on me"
 constexpr int32_t kDead = INT32_MIN;   // wait_counter: gave up (watchdog / error word)
 
@@ -128,17 +128,46 @@ struct Lay {
     static constexpr int kBytes = kCtl + (kStripWord + 4) * 4;
     // store waves per compute wave, rows per store-wave batch (kSPR batches in
     // flight <= 64 rows of ring slack)
+    // C == 1 rings are GROUPED: a lane keeps 4 steps' results and writes them as
+    // one 16-byte record (ds_write_b128 per 4 steps instead of ds_write_b32 per
+    // step); group g = step / 4 of the ring holds the 64 lanes' records, lane l
+    // at record slot gpos(l) (grp_pos below)
+    static constexpr bool kGrp = C == 1;
 #ifdef NW_SPR
     static constexpr int kSPR = NW_SPR;  // (tuning builds: make variant DEFS=-DNW_SPR=3)
 #else
-    static constexpr int kSPR = C == 4 ? 3 : 2;
+    static constexpr int kSPR = C == 4 ? 3 : C == 1 ? 1 : 2;
 #endif
+#ifdef NW_BATCH
+    static constexpr int kBatch = NW_BATCH;
+#else
     static constexpr int kBatch = C == 4 ? 8 : 16;
+#endif
     static constexpr int kWaves = NC * (1 + kSPR);
     // compute wave: check ring space every kChk steps, publish progress every kPub
+    // (the ring's 64 slots of slack are eaten by these granularities: a batch,
+    // the check period plus the staleness of the counter it uses, the publish
+    // period -- keep them small)
+#ifdef NW_CHK
+    static constexpr int kChk = NW_CHK;
+#else
     static constexpr int kChk = 16;
+#endif
     static constexpr int kPub = 8;
 };
+// Record slot of compute lane a inside a group of a grouped ring: a rotation
+// within each 8-lane block, gpos(a) = 8*(a/8) + (a + a/8) % 8.  It keeps both
+// sides conflict-free:
+//   * ds_write_b128 (lanes served in blocks of 8): gpos % 8 = (a + a/8) % 8 is
+//     distinct over a block, so the block covers all 32 banks;
+//   * a store wave reads 8 rows x 32 columns per store instruction with
+//     ds_read_b32 (two 32-lane halves): half-lane (r, q) (row f+r, r < 4 within
+//     the half, q < 8) reads column a = 32h + 4q + k at step f + r + a, bank
+//     4 * (gpos(a) % 8) + (f + r + k) % 4; gpos(a) % 8 is distinct over q (a/8
+//     steps once per two q while 4q % 8 alternates) and (f + r + k) % 4 over r,
+//     so the 32 lanes hit 32 banks.
+__device__ __forceinline__ uint32_t grp_pos(uint32_t a) { return (a & ~7u) | ((a + (a >> 3)) & 7u); }
+
 static_assert(Lay<4, 1>::kBytes <= 160 * 1024, "ring must fit a CU's LDS");
 static_assert(Lay<2, 2>::kBytes <= 160 * 1024, "ring must fit a CU's LDS");
 static_assert(Lay<1, 4>::kBytes <= 160 * 1024, "ring must fit a CU's LDS");
@@ -163,7 +192,7 @@ __device__ __forceinline__ void ctr_store(int32_t *p, int32_t v) {
 
 // Slow path of the hand-off: re-poll the granules of one 64-row block until
 // those of chunk c (lanes 16c .. 16c+15) carry `tag` (s_sleep between polls).
-// Bounded: gives up -- raising the error word -- after kTimeoutTicks, or at once
+// Bounded: gives up -- raising the error word -- after `tmo` ticks, or at once
 // if another wave already raised it.  Returns the last value read; the caller
 // re-checks its tag.
 //
@@ -175,7 +204,7 @@ __device__ __forceinline__ void ctr_store(int32_t *p, int32_t v) {
 // drains the counters on the slow path only (the callee's entry waits), so the
 // fast path keeps counted vmcnt(N) waits.
 __device__ __noinline__ uint64_t wait_chunk(const uint64_t *g, uint32_t tag, int c,
-                                            uint32_t *ctrl, uint32_t site) {
+                                            uint32_t *ctrl, uint32_t site, uint64_t tmo) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     const int lane = threadIdx.x & 63;
     const bool in_chunk = (lane >> 4) == c;
@@ -184,7 +213,7 @@ __device__ __noinline__ uint64_t wait_chunk(const uint64_t *g, uint32_t tag, int
         const uint64_t v = gran_load(g);
         if (__all(!in_chunk || (uint32_t)(v >> 32) == tag)) return v;
         if (ctrl_load(ctrl + 1) != 0u) return v;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > kTimeoutTicks) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > tmo) {
             give_up(ctrl, 1u, site, g, tag, (int64_t)(v >> 32));
             return v;
         }
@@ -202,27 +231,32 @@ __device__ __forceinline__ int chunks_ready(uint64_t v, uint32_t tag) {
 }
 
 // Bounded spin until the LDS counter *p reaches `need`; returns the value seen
-// (kDead once the error word is raised or the watchdog expires).  Slow path of
-// wait_counter (out of line: see wait_chunk).
-__device__ __noinline__ int32_t wait_counter_slow(const int32_t *p, int32_t need, uint32_t *ctrl,
-                                                  uint32_t site) {
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    for (;;) {
-        const int32_t v = __builtin_amdgcn_readfirstlane(ctr_load(p));
-        if (v >= need) return v;
-        if (ctrl_load(ctrl + 1) != 0u) return kDead;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > kTimeoutTicks) {
-            give_up(ctrl, 3u, site, p, need, v);
-            return kDead;
-        }
-        __builtin_amdgcn_s_sleep(1);
-    }
+// (kDead once the watchdog expires).  The loop touches only LDS: a global memory
+// access in it would make the compiler drain every store and prefetch the wave
+// has in flight (s_waitcnt vmcnt(0)) each time it waits -- for a store wave, the
+// whole point of having stores in flight -- and a scalar poll of the error word
+// from every wave of the chip at once slows the fill a hundredfold (measured).
+// A wave that gives up releases the waves waiting on it anyway: compute_strip
+// and store_strip publish kDone on every exit path.
+__device__ __noinline__ void wait_expired(uint32_t *ctrl, uint32_t site, const int32_t *p, int32_t need,
+                                          int32_t seen) {
+    give_up(ctrl, 3u, site, p, need, seen);
 }
 __device__ __forceinline__ int32_t wait_counter(const int32_t *p, int32_t need, uint32_t *ctrl,
-                                             uint32_t site) {
-    const int32_t v = __builtin_amdgcn_readfirstlane(ctr_load(p));
+                                             uint32_t site, uint64_t tmo) {
+    int32_t v = __builtin_amdgcn_readfirstlane(ctr_load(p));
     if (v >= need) return v;
-    return __builtin_amdgcn_readfirstlane(wait_counter_slow(p, need, ctrl, site));
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        __builtin_amdgcn_s_sleep(1);
+        v = __builtin_amdgcn_readfirstlane(ctr_load(p));
+        if (v >= need) return v;
+        // twice the hand-off bound: a partner in the workgroup only stalls behind
+        // a hand-off or halo wait, and that wait must be the one that reports
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 2 * tmo) break;
+    }
+    wait_expired(ctrl, site, p, need, v);
+    return kDead;
 }
 
 // Rows every store wave of a ring has read out of it (each publishes the
@@ -235,9 +269,9 @@ __device__ __forceinline__ int32_t rows_read(const int32_t *rd) {
     return v;
 }
 template <int NS>
-__device__ __forceinline__ void wait_rows_read(const int32_t *rd, int32_t need, uint32_t *ctrl) {
+__device__ __forceinline__ void wait_rows_read(const int32_t *rd, int32_t need, uint32_t *ctrl, uint64_t tmo) {
 #pragma unroll
-    for (int q = 0; q < NS; ++q) (void)wait_counter(rd + q, need, ctrl, 1);
+    for (int q = 0; q < NS; ++q) (void)wait_counter(rd + q, need, ctrl, 1, tmo);
 }
 
 // Row characters of local iteration j (steps 64j .. 64j+63): lane l needs the
@@ -317,7 +351,8 @@ struct Lanes {
     uint32_t thi[C];
     int32_t cb;        // last value read of the store waves' row counters
     uint32_t rb[2];    // ring byte address of this lane's piece of slot 0 / 64
-    uint32_t rc[2];    // read-back address of the right column (see run_iter)
+    uint32_t rc[2];    // read-back address of the right column (see run_iter); grouped
+                       // rings: rc[0] = record of lane 63, rc[1] = (lane & 15) - 1
     int32_t rcol;      // right-column value read back, published a few steps later
 };
 
@@ -344,6 +379,7 @@ struct Feed {
     bool dead;
     bool trace_pub;      // debug trace: stamp the publish of chunk 0 in this iteration
     uint64_t tpub;
+    uint64_t tmo;        // watchdog bound (FillArgs::timeout_ticks)
 };
 
 // Where a compute wave's right column goes.
@@ -387,6 +423,7 @@ __device__ __forceinline__ void run_iter(char *__restrict__ lds, int it, const u
     asm volatile("" : "+v"(rbase));
     rbase &= 0x3FFFFu;
     char *ringw = lds + rbase;
+    int32_t gq[4];  // grouped rings: results of the current 4-step group
     // publish chunk c of block b (lanes i < 16 hold rows 64b + 16c + i)
     auto publish = [&](int c) {
         if (b < 0) return;
@@ -407,7 +444,7 @@ __device__ __forceinline__ void run_iter(char *__restrict__ lds, int it, const u
             const int32_t need = s0 + 4 * g + L::kChk - kR;
             if (__builtin_amdgcn_readfirstlane(S.cb) < need) {
                 const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
-                wait_rows_read<L::kSPR>(rd, need, ctrl);
+                wait_rows_read<L::kSPR>(rd, need, ctrl, F.tmo);
                 F.rticks += __builtin_amdgcn_s_memrealtime() - w0;  // (trace: ring back-pressure)
             }
             S.cb = rows_read<L::kSPR>(rd);  // for the next check (kChk steps on)
@@ -420,11 +457,11 @@ __device__ __forceinline__ void run_iter(char *__restrict__ lds, int it, const u
             if (F.ready <= c) {
                 const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
                 if (F.src == FEED_GRAN) {
-                    const uint64_t v = wait_chunk(F.g, F.tag, c, ctrl, 2);
+                    const uint64_t v = wait_chunk(F.g, F.tag, c, ctrl, 2, F.tmo);
                     F.dead |= !__all((lane >> 4) != c || (uint32_t)(v >> 32) == F.tag);
                     if ((lane >> 4) == c) F.ring[((it & 3) << 6) + lane] = (int32_t)(uint32_t)v;
                 } else {
-                    F.dead |= wait_counter(F.pub, s0 + 16 * (c + 1), ctrl, 3) == kDead;
+                    F.dead |= wait_counter(F.pub, s0 + 16 * (c + 1), ctrl, 3, F.tmo) == kDead;
                     lds_order();  // feed reads after the counter that published them
                 }
                 F.nslow += 1;
@@ -455,6 +492,7 @@ __device__ __forceinline__ void run_iter(char *__restrict__ lds, int it, const u
                 act = S.rr >= 1;
             }
             VT tv;
+            (void)tv;
             static_for<0, C>([&](auto kc) {
                 constexpr int k = decltype(kc)::value;
                 const uint32_t w = MODE == SUB_PERM ? sc[k] : word;
@@ -466,20 +504,37 @@ __device__ __forceinline__ void run_iter(char *__restrict__ lds, int it, const u
                 if constexpr (RAMP) x = act ? x : S.u[k];
                 S.u[k] = x;
                 left = x;
-                set_comp<C>(tv, k, x);
+                if constexpr (L::kGrp) {
+                    gq[u & 3] = x;
+                } else {
+                    set_comp<C>(tv, k, x);
+                }
             });
-            *(VT *)(ringw + u * L::kSlot) = tv;  // ring slot 64*HALF + u
+            if constexpr (!L::kGrp) {
+                *(VT *)(ringw + u * L::kSlot) = tv;  // ring slot 64*HALF + u
+            } else if constexpr ((u & 3) == 3) {
+                // group 16*HALF + u/4: this lane's record of steps u-3 .. u
+                *(int4 *)(ringw + (u >> 2) * (64 * 16)) = make_int4(gq[0], gq[1], gq[2], gq[3]);
+            }
             // right column of block b, chunk c = u / 16: read back after the
-            // step that completed it, publish three steps later
-            if constexpr ((u & 15) == 14) {
+            // step that completed it (grouped: after its record is written),
+            // publish three steps later
+            if constexpr ((u & 15) == (L::kGrp ? 15 : 14)) {
                 constexpr int c = u >> 4;
-                // lane i < 16: slot (64*HALF + 16c + i - 1) mod kR, lane 63's last column
-                const uint32_t a = (HALF == 0 && c == 0) ? S.rc[0] : S.rc[1] + (64 * HALF + 16 * c) * L::kSlot;
+                uint32_t a;
+                if constexpr (L::kGrp) {
+                    // lane i < 16: step 64*HALF + 16c + i - 1 (mod kR) of lane 63
+                    const uint32_t t = (uint32_t)(64 * HALF + 16 * c + (int)S.rc[1]) & (uint32_t)(kR - 1);
+                    a = S.rc[0] + (t >> 2) * (64 * 16) + (t & 3u) * 4u;
+                } else {
+                    // lane i < 16: slot (64*HALF + 16c + i - 1) mod kR, lane 63's last column
+                    a = (HALF == 0 && c == 0) ? S.rc[0] : S.rc[1] + (64 * HALF + 16 * c) * L::kSlot;
+                }
                 S.rcol = *(const int32_t *)(lds + a);
             }
-            if constexpr ((u & 15) == 1 && u > 16) {
+            if constexpr ((u & 15) == (L::kGrp ? 2 : 1) && u > 16) {
                 publish((u >> 4) - 1);
-                if constexpr (u == 17) {
+                if constexpr (u == 16 + (L::kGrp ? 2 : 1)) {
                     if (F.trace_pub) F.tpub = __builtin_amdgcn_s_memrealtime();
                 }
             }
@@ -530,7 +585,7 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
             ok &= (uint32_t)(g0 >> 32) == A.halo_tag;
             if (__all(ok)) break;
             if (ctrl_load(A.ctrl + 1) != 0u) { dead = true; break; }
-            if (__builtin_amdgcn_s_memrealtime() - h0 > kTimeoutTicks) {
+            if (__builtin_amdgcn_s_memrealtime() - h0 > A.timeout_ticks) {
                 give_up(A.ctrl, 2u, 4, A.halo_in, A.halo_tag, 0);
                 dead = true;
                 break;
@@ -566,12 +621,19 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
     S.rr = -lane - 1;
     S.cb = 0;
     S.rcol = 0;
-    S.rb[0] = (uint32_t)(j * L::kRing) + (uint32_t)lane * (4u * C);
+    if constexpr (L::kGrp) {
+        S.rb[0] = (uint32_t)(j * L::kRing) + grp_pos((uint32_t)lane) * 16u;
+    } else {
+        S.rb[0] = (uint32_t)(j * L::kRing) + (uint32_t)lane * (4u * C);
+    }
     S.rb[1] = S.rb[0] + 64u * L::kSlot;
     // right-column read-back: lane i < 16 reads slot (64*HALF + 16c + i - 1) mod kR
     // at lane 63's last column (byte kSlot - 4 of the slot).  rc[1] + offset
     // covers every (HALF, c) but (0, 0), whose lane 0 wraps to slot kR - 1: rc[0].
-    {
+    if constexpr (L::kGrp) {
+        S.rc[0] = (uint32_t)(j * L::kRing) + grp_pos(63u) * 16u;
+        S.rc[1] = (uint32_t)((lane & 15) - 1);
+    } else {
         const int i = lane & 15;
         S.rc[1] = (uint32_t)(j * L::kRing + i * L::kSlot - 4);  // (i - 1) * kSlot + kSlot - 4
         S.rc[0] = i == 0 ? (uint32_t)(j * L::kRing + L::kRing - 4) : S.rc[1];
@@ -593,6 +655,7 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
     F.dead = dead;  // (a halo wait may already have given up)
     F.trace_pub = false;
     F.tpub = 0;
+    F.tmo = A.timeout_ticks;
     Out O;
     O.lds = j + 1 < NC;
     O.ring = (int32_t *)(lds + L::kFeed) + (j + 1 < NC ? j + 1 : j) * kFeedRows;
@@ -644,7 +707,7 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
         }
         // feed-ring space for this iteration's publish (rows of block it-1 land
         // where rows of block it-5 were): wave j+1 must have finished it-5
-        if (O.lds && it >= 5) F.dead |= wait_counter(next_done, it - 4, A.ctrl, 5) == kDead;
+        if (O.lds && it >= 5) F.dead |= wait_counter(next_done, it - 4, A.ctrl, 5, A.timeout_ticks) == kDead;
         F.ready = 4;
         if (it < nblocks) {
             if (F.src == FEED_GRAN) {
@@ -654,7 +717,7 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
                 if (F.ready == 0) {  // chunk 0 is needed right away
                     const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
                     if (traced) twait = w0;
-                    gv = wait_chunk(F.g, F.tag, 0, A.ctrl, 6);
+                    gv = wait_chunk(F.g, F.tag, 0, A.ctrl, 6, A.timeout_ticks);
                     F.dead |= !__all((lane >> 4) != 0 || (uint32_t)(gv >> 32) == F.tag);
                     F.nslow += 1;
                     F.wticks += __builtin_amdgcn_s_memrealtime() - w0;
@@ -666,7 +729,7 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
                 if (pv < it * 64 + 16) {
                     const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
                     if (traced) twait = w0;
-                    pv = wait_counter(F.pub, it * 64 + 16, A.ctrl, 7);
+                    pv = wait_counter(F.pub, it * 64 + 16, A.ctrl, 7, A.timeout_ticks);
                     F.dead |= pv == kDead;
                     F.nslow += 1;
                     F.wticks += __builtin_amdgcn_s_memrealtime() - w0;
@@ -804,7 +867,7 @@ __device__ __forceinline__ void store_strip(const FillArgs &A, char *__restrict_
         const int32_t want = min(f + BATCH, nrows);
         if (avail < want) {
             int32_t sa = __builtin_amdgcn_readfirstlane(ctr_load(ctr));
-            if (sa != kDone && sa - 63 < want) sa = wait_counter(ctr, want + 63, A.ctrl, 8);
+            if (sa != kDone && sa - 63 < want) sa = wait_counter(ctr, want + 63, A.ctrl, 8, A.timeout_ticks);
             avail = (sa == kDone || sa == kDead) ? nrows : min(sa - 63, nrows);
             lds_order();  // ring reads after the counter that released them
             if (bcol) bnd0 = *bnd0p;
@@ -831,6 +894,10 @@ __device__ __forceinline__ void store_strip(const FillArgs &A, char *__restrict_
         for (int m = 0; m < NR; ++m) pa[m] = adv(pa[m], (NS - 1) * BATCH);  // skip the others'
 #pragma unroll
         for (int e = 0; e < 4; ++e) kc[e] += ug * (uint32_t)(NS * BATCH);
+        // the batch is in registers: release its ring slots before the stores
+        // (in-order LDS: the counter is written after the reads have read)
+        lds_order();
+        ctr_store(mine, f + NS * BATCH);
         if (want - f == BATCH) {
 #pragma unroll
             for (int g = 0; g < NG; ++g)
@@ -850,8 +917,6 @@ __device__ __forceinline__ void store_strip(const FillArgs &A, char *__restrict_
             }
         }
         rowp += NS * BATCH * rowb;
-        lds_order();
-        ctr_store(mine, f + NS * BATCH);  // my rows below are out of the ring
     }
     ctr_store(mine, kDone);
     // Row band: hand this ring's columns of the last row (n2) to the next band.
@@ -872,6 +937,185 @@ __device__ __forceinline__ void store_strip(const FillArgs &A, char *__restrict_
                 __hip_atomic_store(A.halo_out + c, ((uint64_t)A.halo_tag << 32) | x,
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
+        }
+        if (bcol && lane == 0)
+            __hip_atomic_store(A.halo_out,
+                               ((uint64_t)A.halo_tag << 32) | (uint32_t)(bnd0 + (int32_t)A.n2 * A.gap),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// Store wave q of compute wave j on strip p, GROUPED ring (C == 1: 64 columns,
+// records of 4 steps, lane slots gpos -- see grp_pos).  One store instruction
+// covers 8 rows x 32 columns: lane (r, q8) = (lane / 8, lane % 8) takes row
+// f + r, columns 32h + 4*q8 .. +3 (h = 0, 1: two instructions per 8 rows),
+// gathered with 4 conflict-free ds_read_b32 (the value of column a of row f + r
+// was computed at step f + r + a: record group (f+r+a)/4, word (f+r+a)%4).
+// Rows go in batches of kBatch dealt round robin to the kSPR store waves.
+template <int NC>
+__device__ __forceinline__ void store_strip_grp(const FillArgs &A, char *__restrict__ lds, int p,
+                                                int j, int q, int lane) {
+    typedef Lay<1, NC> L;
+    constexpr int BATCH = L::kBatch;  // a multiple of 8
+    constexpr int NS = L::kSPR;
+    constexpr int NU = BATCH / 8;     // 8-row units per batch
+    constexpr uint32_t kMask = (uint32_t)L::kRing - 1u;
+    int32_t *ctr = (int32_t *)(lds + L::kCtl) + j * L::kCtlWords;
+    const uint32_t ring0 = (uint32_t)(j * L::kRing);
+    const int64_t c0 = A.col0 + (int64_t)p * (NC * 64) + (int64_t)j * 64;
+    const int32_t nrows = (int32_t)(A.n2 + 1);
+    const bool timing = (A.flags & 1) != 0;
+    const int ro = lane >> 3, cq = lane & 7;
+    const int64_t rowb = timing ? 0 : A.pitch * 4;
+    char *scr = (char *)(A.scratch + (int64_t)blockIdx.x * kScratchWords);
+    const int32_t f0 = q * BATCH;
+    const uint32_t ug = (uint32_t)A.gap;
+    // ring byte offset (within the ring) of column a = 32h + 4cq + k of row f0 + ro,
+    // and kc = GAP * (row + column) of it (the ring holds w = t - GAP*(i+j))
+    uint32_t pa[2][4], kc[2][4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t a = (uint32_t)(32 * h + 4 * cq + k);
+            const uint32_t st = (uint32_t)(f0 + ro) + a;
+            pa[h][k] = (((st >> 2) * 1024u) & kMask) + grp_pos(a) * 16u + (st & 3u) * 4u;
+            kc[h][k] = ug * (uint32_t)(f0 + ro) + ug * (uint32_t)(c0 + a);
+        }
+    // the last strip may overhang the pitch: store only 16-byte pieces wholly inside the row
+    bool col_ok[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) col_ok[h] = c0 + 32 * h + 4 * cq + 4 <= A.pitch;
+    char *rowp = timing ? scr : (char *)(A.table + c0) + (int64_t)f0 * rowb;
+    const uint32_t voff = (uint32_t)(ro * rowb) + (uint32_t)cq * 16u;
+    const bool bcol = A.col0 != 0 && p == 0 && j == 0 && !timing;
+    int32_t bnd0 = 0;
+    const int32_t *bnd0p = (const int32_t *)(lds + L::kCtl) + L::kStripWord + 1;
+    int32_t *mine = ctr + 3 + q;
+    if (A.flags & 8) {  // debug: no store waves at all (compute-pace probe, timing only)
+        ctr_store(mine, kDone);
+        return;
+    }
+    // debug trace (store wave 0 of ring 0): cycles waiting for rows / issuing stores
+    const bool trace = A.trace != nullptr && j == 0 && q == 0;
+    uint64_t tw = 0, ts = 0;
+    int32_t avail = 0;
+    // rows f .. f+BATCH-1 complete in the ring (bounded wait)
+    auto wait_rows = [&](int32_t f) {
+        const int32_t want = min(f + BATCH, nrows);
+        if (avail < want) {
+            const uint64_t t0 = trace ? __builtin_amdgcn_s_memtime() : 0;
+            int32_t sa = __builtin_amdgcn_readfirstlane(ctr_load(ctr));
+            if (sa != kDone && sa - 63 < want) sa = wait_counter(ctr, want + 63, A.ctrl, 8, A.timeout_ticks);
+            avail = (sa == kDone || sa == kDead) ? nrows : min(sa - 63, nrows);
+            lds_order();
+            if (bcol) bnd0 = *bnd0p;
+            if (trace) tw += __builtin_amdgcn_s_memtime() - t0;
+        }
+    };
+    // the next batch from the ring into v (the LDS reads are only issued here;
+    // the stores of the previous batch go out while they are in flight)
+    auto read_batch = [&](u32x4 (&v)[NU][2]) {
+#pragma unroll
+        for (int g = 0; g < NU; ++g)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t x = *(const uint32_t *)(lds + ring0 + ((pa[h][k] + g * 2048u) & kMask));
+                    v[g][h][k] = x + kc[h][k] + ug * (uint32_t)(8 * g);
+                }
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                pa[h][k] = (pa[h][k] + (uint32_t)(NS * BATCH / 4) * 1024u) & kMask;
+                kc[h][k] += ug * (uint32_t)(NS * BATCH);
+            }
+    };
+    // stores of batch f (v from read_batch); its ring slots are released first
+    auto store_batch = [&](int32_t f, const u32x4 (&v)[NU][2]) {
+        // (in-order LDS: this counter store executes after the batch's reads)
+        lds_order();
+        ctr_store(mine, f + NS * BATCH);
+        const uint64_t t0 = trace ? __builtin_amdgcn_s_memtime() : 0;
+        char *rp = rowp + (int64_t)(f - f0) * rowb;
+        if (min(f + BATCH, nrows) - f == BATCH) {
+#pragma unroll
+            for (int g = 0; g < NU; ++g)
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    if (col_ok[h]) *(u32x4 *)(rp + (int64_t)g * 8 * rowb + voff + h * 128) = v[g][h];
+        } else {
+#pragma unroll
+            for (int g = 0; g < NU; ++g)
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    if (col_ok[h] && f + g * 8 + ro < nrows)
+                        *(u32x4 *)(rp + (int64_t)g * 8 * rowb + voff + h * 128) = v[g][h];
+        }
+        if (bcol) {
+#pragma unroll
+            for (int g = 0; g < NU; ++g) {
+                const int32_t r = f + g * 8 + ro;
+                if (cq == 0 && r < nrows)
+                    *(int32_t *)(rp + (int64_t)g * 8 * rowb + (int64_t)voff - 4) = bnd0 + r * A.gap;
+            }
+        }
+        if (trace) ts += __builtin_amdgcn_s_memtime() - t0;
+    };
+    constexpr int32_t D = NS * BATCH;
+    // Deadlock freedom of the pipeline: before storing batch f a store wave
+    // waits for batch f + D, i.e. for step f + D + BATCH - 1 + 63, while the
+    // rows it has released stop at f; the compute wave writes that step only
+    // once rows <= step + kChk - kR are read.
+    static_assert(D + BATCH - 1 + 63 + L::kChk - kR <= 0, "store pipeline lookahead exceeds the ring");
+    if (A.flags & 4) {  // debug: drain the ring without reading it
+        for (int32_t f = f0; f < nrows; f += D) {
+            wait_rows(f);
+            lds_order();
+            ctr_store(mine, f + D);
+        }
+    } else if (f0 < nrows) {
+        // software pipeline over two register sets: batch f + D is read while
+        // batch f is stored
+        u32x4 va[NU][2], vb[NU][2];
+        wait_rows(f0);
+        read_batch(va);
+        for (int32_t f = f0;; f += 2 * D) {
+            if (f + D >= nrows) {
+                store_batch(f, va);
+                break;
+            }
+            wait_rows(f + D);
+            read_batch(vb);
+            store_batch(f, va);
+            if (f + 2 * D >= nrows) {
+                store_batch(f + D, vb);
+                break;
+            }
+            wait_rows(f + 2 * D);
+            read_batch(va);
+            store_batch(f + D, vb);
+        }
+    }
+    ctr_store(mine, kDone);
+    if (trace && lane == 0) {
+        uint64_t *trw = A.trace + (int64_t)p * kTraceWords;
+        trw[16] = tw;
+        trw[17] = 0;
+        trw[18] = ts;
+    }
+    // Row band: hand this ring's 64 columns of the last row to the next band (see store_strip)
+    if (A.halo_out != nullptr && ((nrows - 1) / BATCH) % NS == q && ctrl_load(A.ctrl + 1) == 0u) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const int32_t *last = A.table + A.n2 * A.pitch;
+        const int64_t c = c0 + lane;
+        if (c <= A.n1) {
+            const uint32_t x = (uint32_t)__hip_atomic_load(last + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(A.halo_out + c, ((uint64_t)A.halo_tag << 32) | x, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
         }
         if (bcol && lane == 0)
             __hip_atomic_store(A.halo_out,
@@ -912,7 +1156,10 @@ __global__ __launch_bounds__((64 * Lay<C, NC>::kWaves)) void nw_fill_strips(Fill
                 compute_strip<C, NC, SUB_GEN>(A, lds, p, wave, lane);
         } else {
             const int b = wave - NC;
-            store_strip<C, NC>(A, lds, p, b % NC, b / NC, lane);
+            if constexpr (L::kGrp)
+                store_strip_grp<NC>(A, lds, p, b % NC, b / NC, lane);
+            else
+                store_strip<C, NC>(A, lds, p, b % NC, b / NC, lane);
         }
         __syncthreads();  // the rings and counters are reused by the next strip
     }

@@ -10,7 +10,7 @@ constexpr int kQOff = 64;          // rowpack index offset (lane l reads index 4
 constexpr int32_t kNeg = -(1 << 29);  // "minus infinity" fed left of column 0
 constexpr int kScratchWords = kWave * kWave + 2 * kWave;  // per workgroup (16.5 KB)
 constexpr int kMaxSub = 4;        // max columns per lane (strip = 64 * C columns)
-constexpr int kTraceWords = 16;    // debug trace words per strip
+constexpr int kTraceWords = 24;    // debug trace words per strip (nw_debug_trace_words)
 constexpr uint32_t kMaxPerm = 7;  // distinct column characters the v_perm score tables cover
 constexpr int kMetaBytes = 256 + 16;  // charmap[256], nprof (+ pad)
 
@@ -49,6 +49,7 @@ struct FillArgs {
     const uint32_t *nprof;
     int32_t match, mismatch, gap;
     int32_t flags;             // debug: bit0 = send table stores to the scratch tile (timing only)
+    uint64_t timeout_ticks;    // bound of every in-kernel wait (s_memrealtime ticks, 100 MHz)
 };
 
 // Launch helpers implemented in nw_fill.hip.  Return hipError_t as int.

@@ -11,7 +11,8 @@ fill kernel (nw_fill_band_async) waits, strip by strip, for its halo granules
 ({tag, value}, one per column) and publishes its own last row, strip by strip, straight
 into the next rank's halo buffer in peer HBM over xGMI (system-scope stores from the
 kernel; the buffer is mapped with HIP IPC).  The halo therefore advances at strip
-granularity (64 columns) with no host round trip and no copy engine, collective or
+granularity (one strip: 64 * C * NC columns, C columns per lane, NC chained compute
+waves) with no host round trip and no copy engine, collective or
 stream-ordered gating on the data path.  torch.distributed (gloo) is the control plane
 only: handle exchange, the per-step barrier and the max-over-ranks timing.
 
@@ -57,19 +58,20 @@ class LocalBands:
                  strip_waves: int = 0):
         import torch
         self.n1, self.n2, self.P, self.device = n1, n2, nbands, device
-        self.substrips = substrips
-        self.strip_waves = strip_waves
         self.layout = plan(n2, nbands)
+        # one shape for every band (auto: the tuned shape for a band of this size)
+        self.substrips, self.strip_waves = nwhip.strip_shape(
+            substrips, strip_waves, n1, max(rows for rows, _ in self.layout) - 1)
         if any(rows < 1 for rows, _ in self.layout):
             raise ValueError(f"{nbands} bands need at least {nbands} rows (n2+1 = {n2 + 1})")
         self.tables = [nwhip.Context.alloc_table(n1, rows - 1) for rows, _ in self.layout]
         self.halos = [None] + [nwhip.Halo(n1, device) for _ in range(nbands - 1)]
         self.ctxs = [nwhip.Context(device) for _ in range(nbands)]
         self.streams = [torch.cuda.Stream(device) for _ in range(nbands)]
-        self.waves = max(1, resident_waves(device, substrips, strip_waves) // nbands)
+        self.waves = max(1, resident_waves(device, self.substrips, self.strip_waves) // nbands)
         self.tag = 0
 
-    def fill(self, d_s1, d_s2, scheme=(1, 0, -1), flags: int = 0) -> int:
+    def fill(self, d_s1, d_s2, scheme=(1, 0, -1), flags: int = 0, timeout_ms: int = 0) -> int:
         """Fill every band; returns the final score t[n2][n1] (last band's last cell)."""
         import torch
         assert int(d_s1.numel()) == self.n1 and int(d_s2.numel()) == self.n2
@@ -82,7 +84,8 @@ class LocalBands:
                 halo_in=self.halos[r].ptr if r > 0 else None,
                 halo_out=self.halos[r + 1].ptr if r + 1 < self.P else None,
                 tag=self.tag, scheme=scheme, waves=self.waves, stream=st, flags=flags,
-                substrips=self.substrips, strip_waves=self.strip_waves)
+                substrips=self.substrips, strip_waves=self.strip_waves, row0=start,
+                timeout_ms=timeout_ms)
         for r, st in enumerate(self.streams):
             s = self.ctxs[r].status(st)
             if s != nwhip.NW_OK:
@@ -148,9 +151,10 @@ def run_bands(args) -> dict | None:
     handles = [None] * world
     dist.all_gather_object(handles, nwhip.ipc_get_handle(halo_in.ptr) if halo_in else None)
     halo_out = nwhip.ipc_open_handle(handles[rank + 1]) if rank + 1 < world else None
+    sub, nc = nwhip.strip_shape(args.substrips, args.strip_waves, n1, rows - 1)
     waves = args.waves
     if args.share_gpu and waves == 0:
-        waves = max(1, resident_waves(dev, args.substrips, args.strip_waves) // world)
+        waves = max(1, resident_waves(dev, sub, nc) // world)
     stream = torch.cuda.current_stream()
     tag = 0
 
@@ -161,7 +165,7 @@ def run_bands(args) -> dict | None:
             ev[0].record(stream)
         ctx.fill_band(s1, s2_band, table, halo_in=halo_in.ptr if halo_in else None,
                       halo_out=halo_out, tag=tag, scheme=scheme, waves=waves, stream=stream,
-                      substrips=args.substrips, strip_waves=args.strip_waves)
+                      substrips=sub, strip_waves=nc, row0=start)
         if ev is not None:
             ev[1].record(stream)
         torch.cuda.synchronize()
@@ -224,7 +228,8 @@ def run_bands(args) -> dict | None:
         "config": {"workload": f"nw_fill_rowbands_{n2}x{n1}", "n1": n1, "n2": n2,
                    "scheme": list(scheme), "band_rows": args.band_rows, "bands": world,
                    "table_bytes": int(table_bytes), "parallelism": f"row bands x{world}",
-                   "halo": "in-kernel xGMI peer stores, 64-column strips",
+                   "halo": f"in-kernel xGMI peer stores, one strip ({64 * sub * nc} columns) at a time",
+                   "strip_shape": [sub, nc],
                    "control_plane": "torch.distributed gloo",
                    "shared_gpu": bool(args.share_gpu)},
         "score": score,

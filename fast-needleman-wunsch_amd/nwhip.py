@@ -29,7 +29,8 @@ EXPORTS = ["nw_params_default", "nw_strerror", "nw_version", "nw_fill", "nw_tabl
            "nw_fill_device", "nw_fill_device_async", "nw_ctx_status", "nw_read_bdna", "nw_free",
            "nw_synth_bdna", "nw_band_layout", "nw_halo_bytes", "nw_fill_band_async",
            "nw_ipc_get_handle", "nw_ipc_open_handle", "nw_ipc_close_handle", "nw_halo_alloc",
-           "nw_halo_free"]
+           "nw_halo_free", "nw_tuned_shape", "nw_debug_ctrl", "nw_debug_set_trace",
+           "nw_debug_trace_words"]
 IPC_HANDLE_BYTES = 64
 
 
@@ -37,7 +38,7 @@ class NwParams(ctypes.Structure):
     _fields_ = [("match", ctypes.c_int32), ("mismatch", ctypes.c_int32), ("gap", ctypes.c_int32),
                 ("mode", ctypes.c_int32), ("waves", ctypes.c_int32), ("device", ctypes.c_int32),
                 ("flags", ctypes.c_int32), ("substrips", ctypes.c_int32),
-                ("strip_waves", ctypes.c_int32)]
+                ("strip_waves", ctypes.c_int32), ("timeout_ms", ctypes.c_int32)]
 
 
 class NwResult(ctypes.Structure):
@@ -50,7 +51,7 @@ class NwResult(ctypes.Structure):
 class NwBand(ctypes.Structure):
     """nw_band (include/nw_hip.h): halo granule buffers of one row band."""
     _fields_ = [("halo_in", ctypes.c_void_p), ("halo_out", ctypes.c_void_p),
-                ("tag", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+                ("tag", ctypes.c_uint32), ("row0", ctypes.c_uint32)]
 
 
 class NwError(RuntimeError):
@@ -125,6 +126,13 @@ def lib() -> ctypes.CDLL:
     L.nw_ipc_close_handle.argtypes = [ctypes.c_void_p]
     L.nw_halo_alloc.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p)]
     L.nw_halo_free.argtypes = [ctypes.c_void_p]
+    L.nw_tuned_shape.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(ctypes.c_int32),
+                                 ctypes.POINTER(ctypes.c_int32)]
+    L.nw_tuned_shape.restype = None
+    L.nw_debug_ctrl.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32)]
+    L.nw_debug_set_trace.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    L.nw_debug_trace_words.argtypes = []
+    L.nw_debug_trace_words.restype = ctypes.c_int32
     _lib = L
     return L
 
@@ -149,7 +157,7 @@ class Scheme:
 
 
 def params(scheme=(1, 0, -1), waves: int = 0, device: int = -1, flags: int = 0,
-           substrips: int = 0, strip_waves: int = 0) -> NwParams:
+           substrips: int = 0, strip_waves: int = 0, timeout_ms: int = 0) -> NwParams:
     if isinstance(scheme, Scheme):
         scheme = (scheme.match, scheme.mismatch, scheme.gap)
     p = NwParams()
@@ -160,6 +168,7 @@ def params(scheme=(1, 0, -1), waves: int = 0, device: int = -1, flags: int = 0,
     p.flags = int(flags)
     p.substrips = int(substrips)
     p.strip_waves = int(strip_waves)
+    p.timeout_ms = int(timeout_ms)
     return p
 
 
@@ -198,6 +207,11 @@ def score(s1, s2, scheme=(1, 0, -1), waves: int = 0, device: int = -1, substrips
     return int(r.score)
 
 
+def trace_words() -> int:
+    """uint64 words per strip of the debug trace (nw_debug_trace_words)."""
+    return int(lib().nw_debug_trace_words())
+
+
 def table_pitch(n1: int) -> int:
     return int(lib().nw_table_pitch(n1))
 
@@ -212,15 +226,23 @@ def table_offset() -> int:
     return int(lib().nw_table_offset())
 
 
-def strip_shape(substrips: int = 0, strip_waves: int = 0) -> tuple[int, int]:
+def tuned_shape(n1: int, n2: int) -> tuple[int, int]:
+    """(C, NC) an auto-shaped fill of an n1 x n2 table uses (nw_tuned_shape)."""
+    c, nc = ctypes.c_int32(), ctypes.c_int32()
+    lib().nw_tuned_shape(n1, n2, ctypes.byref(c), ctypes.byref(nc))
+    return int(c.value), int(nc.value)
+
+
+def strip_shape(substrips: int = 0, strip_waves: int = 0, n1: int = -1, n2: int = -1) -> tuple[int, int]:
     """(C, NC) the library uses for these nw_params values (0 = auto), as
-    make_shape in nw_capi.cpp: auto = (2, 2); C alone implies 256-column strips."""
+    make_shape in nw_capi.cpp: auto = the tuned shape for the table size (n1, n2;
+    (2, 2) when no size is given); C alone implies 256-column strips."""
+    if substrips <= 0 and strip_waves <= 0:
+        return tuned_shape(n1, n2) if n1 >= 0 and n2 >= 0 else (2, 2)
     c = substrips if substrips > 0 else 2
     if strip_waves > 0:
         return c, strip_waves
-    if substrips > 0:
-        return c, {1: 4, 2: 2, 4: 1}[c]
-    return c, 2
+    return c, {1: 4, 2: 2, 4: 1}[c]
 
 
 def strip_lds_bytes(substrips: int, strip_waves: int) -> int:
@@ -342,7 +364,8 @@ class Context:
         return flat[shift:shift + rows * pitch].view(rows, pitch)
 
     def fill(self, d_s1, d_s2, table, scheme=(1, 0, -1), waves: int = 0, stream=None,
-             sync: bool = True, flags: int = 0, substrips: int = 0, strip_waves: int = 0):
+             sync: bool = True, flags: int = 0, substrips: int = 0, strip_waves: int = 0,
+             timeout_ms: int = 0):
         """d_s1/d_s2: int8/uint8 CUDA tensors; table: from alloc_table.  Returns NwResult
         when sync, else None (launch only)."""
         import torch
@@ -352,7 +375,7 @@ class Context:
         if stream is None:
             stream = torch.cuda.current_stream(table.device)
         sp = ctypes.c_void_p(stream.cuda_stream)
-        p = params(scheme, waves, self.device, flags, substrips, strip_waves)
+        p = params(scheme, waves, self.device, flags, substrips, strip_waves, timeout_ms)
         args = (self._h, ctypes.c_void_p(d_s1.data_ptr() if n1 else 0), n1,
                 ctypes.c_void_p(d_s2.data_ptr() if n2 else 0), n2, ctypes.byref(p),
                 ctypes.c_void_p(table.data_ptr()), table.shape[1], sp)
@@ -369,11 +392,13 @@ class Context:
 
     def fill_band(self, d_s1, d_s2_band, table, halo_in=None, halo_out=None, tag: int = 1,
                   scheme=(1, 0, -1), waves: int = 0, stream=None, flags: int = 0,
-                  substrips: int = 0, strip_waves: int = 0) -> None:
+                  substrips: int = 0, strip_waves: int = 0, row0: int = 0,
+                  timeout_ms: int = 0) -> None:
         """Launch one row band (asynchronous).  d_s2_band: the band's side
         characters (len = band rows - 1); table: alloc_table(n1, len(d_s2_band)),
-        row 0 = the halo row.  halo_in / halo_out: int64 CUDA tensors of
-        n1+1 granules or raw device addresses (peer memory from ipc_open_handle)."""
+        row 0 = the halo row, global row `row0` (nw_band_layout start).  halo_in /
+        halo_out: int64 CUDA tensors of n1+1 granules or raw device addresses (peer
+        memory from ipc_open_handle)."""
         import torch
         n1, n2 = int(d_s1.numel()), int(d_s2_band.numel())
         assert table.dtype == torch.int32 and table.is_contiguous()
@@ -388,8 +413,8 @@ class Context:
             return x.data_ptr()
         if stream is None:
             stream = torch.cuda.current_stream(table.device)
-        b = NwBand(addr(halo_in), addr(halo_out), int(tag), 0)
-        p = params(scheme, waves, self.device, flags, substrips, strip_waves)
+        b = NwBand(addr(halo_in), addr(halo_out), int(tag), int(row0))
+        p = params(scheme, waves, self.device, flags, substrips, strip_waves, timeout_ms)
         st = lib().nw_fill_band_async(self._h, ctypes.c_void_p(d_s1.data_ptr() if n1 else 0), n1,
                                       ctypes.c_void_p(d_s2_band.data_ptr() if n2 else 0), n2,
                                       ctypes.byref(p), ctypes.byref(b),
@@ -399,11 +424,19 @@ class Context:
             raise NwError(st, "nw_fill_band_async")
 
     def set_trace(self, trace_tensor) -> None:
-        """Debug: record {start, end, slow waits, wait ticks, t(quarter), t(mid)}
-        per strip into a uint64/int64 CUDA tensor of nstrips*8 elements (None = off)."""
-        L = lib()
-        L.nw_debug_set_trace.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-        L.nw_debug_set_trace(self._h, ctypes.c_void_p(trace_tensor.data_ptr() if trace_tensor is not None else 0))
+        """Debug: per-strip timeline (start, end, waits, ...: tools/trace_strips.py) into
+        a uint64/int64 CUDA tensor of at least strips * trace_words() elements (None = off)."""
+        if trace_tensor is not None:
+            assert trace_tensor.element_size() == 8
+        lib().nw_debug_set_trace(self._h, ctypes.c_void_p(trace_tensor.data_ptr() if trace_tensor is not None else 0))
+
+    def debug_ctrl(self) -> list[int]:
+        """The 8 control words of the last launch (include/nw_hip.h nw_debug_ctrl)."""
+        out = (ctypes.c_uint32 * 8)()
+        st = lib().nw_debug_ctrl(self._h, out)
+        if st != NW_OK:
+            raise NwError(st, "nw_debug_ctrl")
+        return list(out)
 
     def status(self, stream=None) -> int:
         import torch

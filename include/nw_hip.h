@@ -63,7 +63,11 @@ typedef struct nw_params {
     int32_t substrips; /* columns per lane C of a compute wave (1, 2 or 4); 0 = auto */
     int32_t strip_waves; /* chained compute waves per strip NC (1, 2 or 4); 0 = auto.
                             A strip is NC * 64 * C columns; supported (C, NC):
-                            (4,1) (2,1) (1,1) (2,2) (1,2) (1,4); auto = (2,2) */
+                            (4,1) (2,1) (1,1) (2,2) (1,2) (1,4); auto = the tuned
+                            shape for the size (nw_tuned_shape) */
+    int32_t timeout_ms;  /* bound of every in-kernel wait (hand-off, halo, ring);
+                            0 = 20000.  A wait that expires makes the fill return
+                            NW_ERR_TIMEOUT instead of hanging the device. */
 } nw_params;
 
 typedef struct nw_result {
@@ -72,7 +76,7 @@ typedef struct nw_result {
     int64_t cells;          /* n1 * n2 inner cells (GCUPS numerator)      */
     double kernel_ms;       /* device time of the fill (HIP events)       */
     double table_bytes;     /* bytes of table stored: 4 * nRows * nCols   */
-    int32_t strips;         /* super-strips swept (substrips*64 columns)  */
+    int32_t strips;         /* strips swept (64 * substrips * strip_waves columns each) */
     int32_t waves;          /* persistent workers launched                */
     int32_t substrips;      /* columns per lane of a compute wave         */
     int32_t strip_waves;    /* compute waves per strip                    */
@@ -100,6 +104,12 @@ int nw_fill(const int8_t *s1, int64_t n1, const int8_t *s2, int64_t n2,
 
 /* Device-resident API ------------------------------------------------------ */
 typedef struct nw_ctx nw_ctx;
+
+/* Strip shape (columns per lane C, chained compute waves NC) that a fill with
+ * nw_params.substrips = strip_waves = 0 uses for an n1 x n2 table: the table
+ * measured by tools/tune.py (the analogue of the reference's block tuner,
+ * src/common/block-tuner.cpp:26-34, src/block-tune.sh). */
+void nw_tuned_shape(int64_t n1, int64_t n2, int32_t *substrips, int32_t *strip_waves);
 
 /* Row pitch (in int32 elements) the library allocates for nCols = n1+1: a
  * multiple of 64 (256-byte rows) with at least 3 columns of slack after column
@@ -154,7 +164,8 @@ int nw_fill_device_async(nw_ctx *ctx, const int8_t *d_s1, int64_t n1,
  * rank r fills a contiguous band of rows whose row 0 is rank r-1's last row (the
  * halo), received in chunks while r-1 is still filling.  Here band r's kernel
  * takes that row from `halo_in` -- granules {tag:32 | value:32}, one per column
- * 0..n1 -- as each 64-column strip starts, and publishes its own last row into
+ * 0..n1 -- as each strip (64 * substrips * strip_waves columns) starts, and
+ * publishes its own last row into
  * `halo_out` (the next band's halo_in, usually peer memory on the next GPU
  * mapped with nw_ipc_open_handle) as each strip finishes: a pipelined halo with
  * no host round trip.  `tag` identifies the launch (> 0, the same value on both
@@ -163,7 +174,8 @@ typedef struct nw_band {
     const uint64_t *halo_in;  /* NULL: row 0 is the boundary j*gap (first band)  */
     uint64_t *halo_out;       /* NULL: last band                                  */
     uint32_t tag;
-    uint32_t reserved;
+    uint32_t row0;            /* global row index of the band's row 0 (nw_band_layout
+                                 `start`): bounds the cell values for the range check */
 } nw_band;
 
 /* Band layout of mpi-horz-driver.cpp:31-32: rows of band r (including its halo
@@ -194,6 +206,17 @@ int nw_ipc_close_handle(void *d_ptr);
 
 /* Check the in-kernel watchdog word of the last launch (syncs the stream). */
 int nw_ctx_status(nw_ctx *ctx, void *stream);
+
+/* Debug hooks (diagnosis, not needed for fills).
+ * nw_debug_ctrl: the 8 control words of the context's last launch: [0] strip
+ *   ticket, [1] error code (0 ok; 1 hand-off granule wait, 2 halo wait, 3 LDS
+ *   counter wait expired), [2] site << 24 | wave << 16 | address bits, [3] the
+ *   value the wait needed, [4] the value it last saw.  Syncs the device.
+ * nw_debug_set_trace: per-strip timeline buffer (device memory of at least
+ *   strips * nw_debug_trace_words() uint64), NULL = off. */
+int nw_debug_ctrl(nw_ctx *ctx, uint32_t *out8);
+int nw_debug_set_trace(nw_ctx *ctx, void *d_trace);
+int32_t nw_debug_trace_words(void);
 
 /* Host helpers ------------------------------------------------------------- */
 

@@ -49,3 +49,18 @@ def pair(golden):
             cache[name] = (read_bdna(e["argv1"]), read_bdna(e["argv2"]))
         return cache[name]
     return get
+
+
+def big_rows(n1: int, n2: int, scheme):
+    """Row-level golden vectors of a full-size synthetic workload
+    (tests/golden/make_big_rows.py): dict with score, last_row, last_col,
+    row_sum, row_wsum -- decoded from the delta-encoded npz."""
+    import numpy as np
+    name = {(1, 0, -1): "shipped", (1, -1, -1): "mm1"}[tuple(scheme)]
+    z = np.load(os.path.join(GOLDEN, f"big_rows_{n1}x{n2}_{name}.npz"))
+    out = {"score": int(z["score"])}
+    with np.errstate(over="ignore"):
+        for k in ("last_row", "last_col", "row_sum", "row_wsum"):
+            d = z[k]
+            out[k] = np.cumsum(d, dtype=d.dtype)
+    return out

@@ -1,0 +1,168 @@
+"""Parity at BASELINE's full sizes (configs 3 and 4), against row-level golden
+vectors from the pinned oracle (tests/golden/make_big_rows.py; the reference
+itself cannot hold these tables in host RAM -- SURVEY.md 8(c)).
+
+Every row of the device table is compared through its (sum, column-weighted sum)
+checksum; the last row and the last column exactly; the final score against
+synth_scores.json.  Recurrence: src/serial/serial.cpp:21-33; band partition:
+src/mpi/mpi-horz-driver.cpp:31-32, mpi-horz.cpp:16-40.
+
+CPU (-m "not gpu"): the golden files decode consistently, agree with
+synth_scores.json, and the 64k file matches the oracle recomputed here.
+GPU (-m gpu): config 3 (262144^2, 275 GB table, one MI355X) under both schemes,
+the 64k/128k squares, and config 4's row-band geometry (524288 columns in 8
+bands of 4096 rows) through LocalBands.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import nwhip
+import oracle
+from conftest import GOLDEN, big_rows
+
+SQUARES = [(65536, (1, 0, -1)), (65536, (1, -1, -1)), (131072, (1, 0, -1)), (131072, (1, -1, -1)),
+           (262144, (1, 0, -1)), (262144, (1, -1, -1))]
+
+
+def synth_scores():
+    with open(os.path.join(GOLDEN, "synth_scores.json")) as f:
+        return json.load(f)
+
+
+# ------------------------------------------------------------------ CPU
+@pytest.mark.parametrize("n,scheme", SQUARES)
+def test_golden_rows_consistent(n, scheme):
+    g = big_rows(n, n, scheme)
+    assert g["last_row"].size == n + 1 and g["last_col"].size == n + 1
+    assert g["row_sum"].size == n + 1 and g["row_wsum"].size == n + 1
+    assert g["score"] == g["last_row"][-1] == g["last_col"][-1]
+    assert g["score"] == synth_scores()[f"{n}:{','.join(map(str, scheme))}"]
+    # row 0 is the boundary j*GAP (serial.cpp:16); column n1 of row i continues it
+    gap = scheme[2]
+    want = sum(j * gap for j in range(n + 1)) % (1 << 64)
+    assert int(g["row_sum"][0]) == want
+    assert g["last_col"][0] == n * gap
+
+
+def test_golden_band_geometry_consistent():
+    g = big_rows(524288, 32767, (1, 0, -1))
+    assert g["last_row"].size == 524289 and g["row_sum"].size == 32768
+    assert g["score"] == g["last_row"][-1] == g["last_col"][-1]
+
+
+def test_golden_64k_rows_match_oracle():
+    """Re-derive the 64k golden file with the oracle here (17 s)."""
+    n, scheme = 65536, (1, 0, -1)
+    g = big_rows(n, n, scheme)
+    sc, lr, lc, rs, rw = oracle.score(oracle.synth(1, n), oracle.synth(2, n), scheme, want_rows=True)
+    assert sc == g["score"]
+    np.testing.assert_array_equal(lr, g["last_row"])
+    np.testing.assert_array_equal(lc, g["last_col"])
+    np.testing.assert_array_equal(rs, g["row_sum"])
+    np.testing.assert_array_equal(rw, g["row_wsum"])
+
+
+# ------------------------------------------------------------------ GPU
+@pytest.fixture(scope="module")
+def torch():
+    import torch as _t
+    if not _t.cuda.is_available():
+        pytest.skip("no GPU")
+    return _t
+
+
+@pytest.fixture(scope="module")
+def ctx(torch):
+    c = nwhip.Context(0)
+    yield c
+    c.close()
+
+
+def row_checksums(torch, tab, rows, n_cols, chunk=256):
+    """(sum, column-weighted sum) per row mod 2^64 (oracle.row_checksums) on the device,
+    `rows` = the table rows to check, in chunks (a few hundred MB of temporaries next
+    to a 275 GB table)."""
+    w = torch.arange(1, n_cols + 1, dtype=torch.int64, device=tab.device)
+    rs, rw = [], []
+    for r0 in range(0, rows, chunk):
+        r1 = min(rows, r0 + chunk)
+        t64 = tab[r0:r1, :n_cols].to(torch.int64)
+        rs.append(t64.sum(dim=1).cpu())
+        rw.append((t64 * w).sum(dim=1).cpu())
+        del t64
+    return (torch.cat(rs).numpy().view(np.uint64), torch.cat(rw).numpy().view(np.uint64))
+
+
+def check_square(torch, ctx, n, schemes, substrips=0, strip_waves=0):
+    torch.cuda.empty_cache()
+    s1 = torch.from_numpy(nwhip.synth(1, n)).cuda()
+    s2 = torch.from_numpy(nwhip.synth(2, n)).cuda()
+    tab = nwhip.Context.alloc_table(n, n)
+    try:
+        for scheme in schemes:
+            g = big_rows(n, n, scheme)
+            r = ctx.fill(s1, s2, tab, scheme, substrips=substrips, strip_waves=strip_waves)
+            assert r.status == 0
+            assert r.score == g["score"]
+            np.testing.assert_array_equal(tab[n, :n + 1].cpu().numpy(), g["last_row"])
+            np.testing.assert_array_equal(tab[:n + 1, n].cpu().numpy(), g["last_col"])
+            rs, rw = row_checksums(torch, tab, n + 1, n + 1)
+            bad = np.flatnonzero((rs != g["row_sum"]) | (rw != g["row_wsum"]))
+            assert bad.size == 0, f"{bad.size} rows differ, first {bad[:5].tolist()} ({scheme})"
+    finally:
+        del tab
+        torch.cuda.empty_cache()
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+def test_config3_256k_every_row(torch, ctx):
+    """BASELINE config 3: 262144 x 262144 on one MI355X, both schemes, every row."""
+    check_square(torch, ctx, 262144, [(1, 0, -1), (1, -1, -1)])
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+@pytest.mark.parametrize("n", [65536, 131072])
+def test_squares_every_row(torch, ctx, n):
+    check_square(torch, ctx, n, [(1, 0, -1), (1, -1, -1)])
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+@pytest.mark.parametrize("strip", [(2, 2), (1, 4), (4, 1)])
+def test_128k_every_row_by_strip_shape(torch, ctx, strip):
+    check_square(torch, ctx, 131072, [(1, 0, -1)], substrips=strip[0], strip_waves=strip[1])
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+def test_config4_band_geometry(torch):
+    """BASELINE config 4's row bands (524288 columns, 8 bands, mpi-horz partition) with
+    4096 rows per band, concurrently on one device through the in-kernel halo hand-off
+    (the 8-GPU run uses the same kernels with the halo in peer HBM): every row of every
+    band against the whole-table golden rows."""
+    import nw_bands
+    n1, n2, P = 524288, 32767, 8
+    g = big_rows(n1, n2, (1, 0, -1))
+    torch.cuda.empty_cache()
+    lb = nw_bands.LocalBands(n1, n2, P)
+    try:
+        score = lb.fill(torch.from_numpy(nwhip.synth(1, n1)).cuda(),
+                        torch.from_numpy(nwhip.synth(2, n2)).cuda())
+        assert score == g["score"]
+        for r, (rows, start) in enumerate(lb.layout):
+            tab = lb.tables[r]
+            rs, rw = row_checksums(torch, tab, rows, n1 + 1)
+            np.testing.assert_array_equal(rs, g["row_sum"][start:start + rows], err_msg=f"band {r}")
+            np.testing.assert_array_equal(rw, g["row_wsum"][start:start + rows], err_msg=f"band {r}")
+            np.testing.assert_array_equal(tab[:rows, n1].cpu().numpy(), g["last_col"][start:start + rows])
+        rows, _ = lb.layout[-1]
+        np.testing.assert_array_equal(lb.tables[-1][rows - 1, :n1 + 1].cpu().numpy(), g["last_row"])
+    finally:
+        lb.close()
+        del lb
+        torch.cuda.empty_cache()

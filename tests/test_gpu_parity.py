@@ -189,6 +189,54 @@ def test_score_range_refused():
     assert nwhip.score(small, small, (4095, -4095, -4095)) == oracle.score(small, small, (4095, -4095, -4095))
 
 
+def test_band_score_range_refused(torch, ctx):
+    """A band's halo row carries global values: the range check uses the band's global
+    row (nw_band.row0), so a band of a table the whole-table path refuses is refused too."""
+    n1, rows = 1000, 100
+    d1 = torch.from_numpy(nwhip.synth(1, n1)).cuda()
+    d2 = torch.from_numpy(nwhip.synth(2, rows)).cuda()
+    tab = nwhip.Context.alloc_table(n1, rows)
+    halo = torch.zeros(n1 + 1, dtype=torch.int64, device="cuda")
+    scheme = (4095, -4095, -4095)  # (4095 + 4095) * (n1 + row0 + rows + 2) >= 2^28 from row0 ~ 31k
+    with pytest.raises(nwhip.NwError) as e:
+        ctx.fill_band(d1, d2, tab, halo_in=halo, tag=1, scheme=scheme, row0=40000)
+    assert e.value.status == nwhip.NW_ERR_ARG
+    ctx.fill_band(d1, d2, tab, halo_in=None, tag=1, scheme=scheme, row0=0)  # accepted
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("strip", [(2, 2), (1, 4)])
+def test_watchdog_reports_timeout(torch, strip):
+    """A band whose halo never arrives (its tag is never written) must not hang the
+    device: every bounded wait gives up after nw_params.timeout_ms, the launch
+    reports NW_ERR_TIMEOUT, and the control words name the wait (code 2: halo wait,
+    site 4, the tag it needed).  Afterwards the same context fills correctly."""
+    c = nwhip.Context(0)
+    try:
+        n1, rows = 64 * 40 + 5, 300
+        s1 = nwhip.synth(3, n1)
+        s2 = nwhip.synth(4, rows)
+        d1, d2 = torch.from_numpy(s1).cuda(), torch.from_numpy(s2).cuda()
+        tab = nwhip.Context.alloc_table(n1, rows)
+        halo = torch.zeros(n1 + 1, dtype=torch.int64, device="cuda")  # tag 0 everywhere
+        import time
+        t0 = time.time()
+        c.fill_band(d1, d2, tab, halo_in=halo, tag=7, timeout_ms=200,
+                    substrips=strip[0], strip_waves=strip[1])
+        assert c.status() == nwhip.NW_ERR_TIMEOUT
+        assert time.time() - t0 < 30
+        w = c.debug_ctrl()
+        assert w[1] == 2                 # halo wait gave up (nw_fill.hip give_up code 2)
+        assert (w[2] >> 24) == 4         # site 4: the halo wait at the start of a strip
+        assert w[3] == 7                 # the tag it needed
+        # the context recovers: a normal fill right after is exact
+        tab2, r = device_fill(torch, c, s1, s2, (1, 0, -1), substrips=strip[0], strip_waves=strip[1])
+        assert r.status == 0
+        np.testing.assert_array_equal(tab2[:rows + 1, :n1 + 1].cpu().numpy(), oracle.fill(s1, s2))
+    finally:
+        c.close()
+
+
 @pytest.mark.parametrize("waves", [1, 2, 3, 5, 8, 17, 64])
 @pytest.mark.parametrize("strip", STRIP_SHAPES)
 def test_worker_count_independent(torch, ctx, waves, strip):

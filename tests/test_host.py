@@ -132,3 +132,16 @@ def test_driver_cli_argument_errors():
     assert r.returncode == 1 and "incorrect number of arguments" in r.stdout
     r = subprocess.run([drv, "/nonexistent/a", "/nonexistent/b"], capture_output=True, text=True)
     assert r.returncode == 1 and "ERROR: no such file /nonexistent/a" in r.stdout
+
+
+def test_tuned_shape_is_supported():
+    """nw_tuned_shape (the tuner's table, csrc/nw_tuned.h) only ever names supported
+    strip shapes, for every size class."""
+    for n in [0, 1, 100, 4096, 32768, 65536, 131072, 262144, 524288]:
+        c, nc = nwhip.tuned_shape(n, n)
+        assert nwhip.strip_lds_bytes(c, nc) > 0, (n, c, nc)
+        assert nwhip.strip_shape(0, 0, n, n) == (c, nc)
+
+
+def test_trace_words_exported():
+    assert nwhip.trace_words() >= 16

@@ -24,7 +24,7 @@ s1 = torch.from_numpy(nwhip.synth(1, n)).cuda()
 s2 = torch.from_numpy(nwhip.synth(2, n)).cuda()
 tab = nwhip.Context.alloc_table(n, n)
 nstrips = (n + 1 + 63) // 64
-tr = torch.zeros(nstrips * 16, dtype=torch.int64, device="cuda")
+tr = torch.zeros(nstrips * 24, dtype=torch.int64, device="cuda")
 for w in [int(x) for x in args.waves.split(",")]:
     ctx.set_trace(None)
     r0 = ctx.fill(s1, s2, tab, waves=w, flags=args.flags, substrips=args.sub, strip_waves=args.nc)
@@ -32,7 +32,7 @@ for w in [int(x) for x in args.waves.split(",")]:
     r = ctx.fill(s1, s2, tab, waves=w, flags=args.flags, substrips=args.sub, strip_waves=args.nc)
     nstrips = r.strips
     ctx.set_trace(None)
-    t = tr[: nstrips * 16].view(nstrips, 16).cpu().numpy().astype(np.float64)
+    t = tr[: nstrips * 24].view(nstrips, 24).cpu().numpy().astype(np.float64)
     if args.save:
         np.save(f"{args.save}_w{w}_k{r.substrips}.npy", t)
     t0 = t[:, 0].min()
@@ -84,5 +84,8 @@ for w in [int(x) for x in args.waves.split(",")]:
     cyc = (t[:, 7] - t[:, 6])
     print(f"  cycles/step inside run_iter: first wave strip0 {t[0,14]/n:.1f} med {np.median(t[:,14])/n:.1f}; "
           f"last wave strip0 {t[0,15]/n:.1f} med {np.median(t[:,15])/n:.1f}; whole strip med {np.median(cyc)/n:.1f}")
-    for q in [0, 1, 2, nstrips // 4, nstrips // 2, nstrips - 2, nstrips - 1]:
-        print(f"   strip {q}: start {st[q]:.1f} end {en[q]:.1f} dur {dur[q]:.1f} slow {t[q,2]:.0f} wait {t[q,3]/100:.1f}")
+    for q in [0, 1, 2, nstrips // 4, nstrips // 4 + 1, nstrips // 2, nstrips - 2, nstrips - 1]:
+        print(f"   strip {q}: start {st[q]:.1f} end {en[q]:.1f} dur {dur[q]:.1f} slow {t[q,2]:.0f} wait {t[q,3]/100:.1f} "
+              f"ringwait first {t[q,11]/100:.0f} last {t[q,12]/100:.0f} lastfeed {t[q,13]/100:.0f} "
+              f"run_iter cyc/step first {t[q,14]/n:.1f} last {t[q,15]/n:.1f} "
+              f"store wave cyc/row wait {t[q,16]/n:.1f} read {t[q,17]/n:.1f} store {t[q,18]/n:.1f}")

@@ -50,6 +50,7 @@ __global__ __launch_bounds__(64) void step_loop(const uint32_t *pkin, int n, int
     F.dead = false;
     F.trace_pub = false;
     F.tpub = 0;
+    F.tmo = 100000000ull * 20ull;
     nw::Out O;
     O.lds = !GRAN;
     O.ring = (int32_t *)(lds + L::kFeed) + (NC > 1 ? nw::kFeedRows : 0);
