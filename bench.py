@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--band-cols", type=int, default=524288, help="N>1: table columns n1")
     ap.add_argument("--share-gpu", action="store_true",
                     help="N>1 rehearsal: every rank on device 0 (co-resident halves)")
+    ap.add_argument("--workload", choices=["nw", "sw"], default="nw",
+                    help="nw: the headline NW fill (config 3); sw: Smith-Waterman + traceback (config 5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-n", type=int, default=32768, help="CPU baseline sample side")
     return ap.parse_args()
@@ -207,8 +209,70 @@ def run_single(args):
     print(json.dumps(out), flush=True)
 
 
+def run_sw(args):
+    """--workload sw: BASELINE config 5, Smith-Waterman fill + best cell + on-device
+    traceback of the 65536 x 65536 synthetic pair (a step = all three), checked
+    against tests/golden/sw_golden.json (the build's CPU restatement: the reference
+    has no local alignment, parity unpinned)."""
+    import hashlib
+    import torch
+    import nwhip
+    scheme = tuple(int(x) for x in args.scheme.split(",")) if args.scheme != "1,0,-1" else (1, -1, -1)
+    n = args.n if args.n != 262144 else 65536
+    torch.cuda.set_device(0)
+    ctx = nwhip.Context(0)
+    s1 = torch.from_numpy(nwhip.synth(1, n)).cuda()
+    s2 = torch.from_numpy(nwhip.synth(2, n)).cuda()
+    tab = nwhip.Context.alloc_table(n, n)
+
+    def step():
+        r = ctx.fill(s1, s2, tab, scheme, substrips=args.substrips, strip_waves=args.strip_waves,
+                     mode=nwhip.MODE_SW)
+        al, ops = ctx.sw_traceback(s1, s2, tab, (r.end_i, r.end_j), scheme)
+        return r, al, ops
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    fills, tbs = [], []
+    for _ in range(args.steps):
+        r, al, ops = step()
+        fills.append(r.kernel_ms)
+        tbs.append(al.traceback_ms)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    gpath = os.path.join(ROOT, "tests", "golden", "sw_golden.json")
+    g = json.load(open(gpath))["synth"].get(f"{n}:{','.join(map(str, scheme))}") if os.path.exists(gpath) else None
+    ok = None
+    if g is not None:
+        ok = (al.score == g["score"] and [al.end_i, al.end_j] == g["end"] and
+              [al.begin_i, al.begin_j] == g["begin"] and hashlib.sha256(ops.tobytes()).hexdigest() == g["ops_sha256"])
+    cells = n * n
+    table_bytes = 4.0 * (n + 1) * (n + 1)
+    fill_ms = sum(fills) / len(fills)
+    out = {"metric": "GCUPS (DP cell updates/s) on NxN Smith-Waterman fill + on-device traceback",
+           "value": round(cells * args.steps / wall / 1e9, 2), "unit": "GCUPS", "n_gpus": 1,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 3),
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int32",
+           "data": "synthetic (i.i.d. uniform {1,2,3,4}, seeds 1/2)",
+           "config": {"workload": f"sw_fill_traceback_{n}x{n}", "n1": n, "n2": n, "scheme": list(scheme),
+                      "parallelism": "single GPU"},
+           "score": al.score, "end": [al.end_i, al.end_j], "begin": [al.begin_i, al.begin_j],
+           "n_ops": int(al.n_ops), "result_ok": ok,
+           "fill_ms_avg": round(fill_ms, 3), "traceback_ms_avg": round(sum(tbs) / len(tbs), 3),
+           "roofline": {"bound": "hbm", "achieved": round(table_bytes / (fill_ms * 1e6), 1), "peak": HBM_PEAK_GBPS,
+                        "unit": "GB/s", "frac": round(table_bytes / (fill_ms * 1e6) / HBM_PEAK_GBPS, 4),
+                        "traffic": None, "basis": "fill kernel (+ locate) only"},
+           "kernel": nwhip.version()}
+    print(json.dumps(out), flush=True)
+
+
 def main():
     args = parse()
+    if args.workload == "sw":
+        run_sw(args)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus > 1 or world > 1:
         from nw_bands import run_bands  # multi-GPU row bands

@@ -36,6 +36,12 @@ struct nw_ctx {
     int last_sub = 0;
     int last_nc = 0;
     uint64_t *trace = nullptr;  // debug: per-strip timestamps (nw_debug_set_trace)
+    int32_t *smax = nullptr;    // SW: per-strip best cell + best / key words
+    size_t smax_cap = 0;
+    uint8_t *ops = nullptr;     // SW traceback ops (device)
+    size_t ops_cap = 0;
+    int64_t *swinfo = nullptr;  // SW traceback info (4 words) + locate key
+    int last_col0 = 0;
 };
 
 namespace {
@@ -116,7 +122,8 @@ bool fits_i8(int32_t x) { return x >= -128 && x <= 127; }
 
 bool valid_params(const nw_params *p) {
     if (!p) return false;
-    if (p->mode != NW_MODE_NW) return false;
+    if (p->mode != NW_MODE_NW && p->mode != NW_MODE_SW) return false;
+    if (p->mode == NW_MODE_SW && p->gap > 0) return false;  // local alignment needs a penalty
     if (p->substrips != 0 && p->substrips != 1 && p->substrips != 2 && p->substrips != 4) return false;
     if (p->strip_waves != 0 && p->strip_waves != 1 && p->strip_waves != 2 && p->strip_waves != 4)
         return false;
@@ -218,6 +225,9 @@ void nw_ctx_destroy(nw_ctx *c) {
     if (c->meta) (void)hipFree(c->meta);
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->ctrl) (void)hipFree(c->ctrl);
+    if (c->smax) (void)hipFree(c->smax);
+    if (c->ops) (void)hipFree(c->ops);
+    if (c->swinfo) (void)hipFree(c->swinfo);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     delete c;
@@ -229,10 +239,16 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
     if (!c || !d_t || n1 < 0 || n2 < 0 || n1 >= INT32_MAX || n2 >= INT32_MAX) return NW_ERR_ARG;
     if ((n1 > 0 && !d_s1) || (n2 > 0 && !d_s2)) return NW_ERR_ARG;
     if (!valid_params(p)) return NW_ERR_ARG;
+    const bool sw = p->mode == NW_MODE_SW;
+    if (sw && band) return NW_ERR_UNSUPPORTED;  // (local alignment: single table, config 5)
     // The kernel holds w = t - GAP*(i+j) in int32 next to a "minus infinity" of
     // -2^29: |w| <= (max|score| + |GAP|) * (i + j) must stay below 2^28, with i the
     // GLOBAL row (a band's halo row carries the values of row band->row0).
-    {
+    // Smith-Waterman cells are plain, in [0, max|score| * (min(n1, n2) + 1)].
+    if (sw) {
+        const long long m = std::max({std::llabs(p->match), std::llabs(p->mismatch), std::llabs(p->gap)});
+        if (m * (long long)(std::min(n1, n2) + 1) >= (1LL << 28)) return NW_ERR_ARG;
+    } else {
         const long long m = std::max({std::llabs(p->match), std::llabs(p->mismatch), std::llabs(p->gap)});
         const long long i_max = (long long)n2 + (band ? (long long)band->row0 : 0);
         if ((m + std::llabs(p->gap)) * (long long)(n1 + i_max + 2) >= (1LL << 28)) return NW_ERR_ARG;
@@ -258,6 +274,7 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
     NW_HIP_TRY(hipSetDevice(c->device));
     const Shape s = make_shape(n1, n2, p->waves, p->substrips, p->strip_waves, c->cus, col0);
     if (!nw::shape_ok(s.K, s.NC)) return NW_ERR_ARG;
+    if (sw && !nw::sw_shape_ok(s.K, s.NC)) return NW_ERR_UNSUPPORTED;
     if (s.nstrips > INT32_MAX / 2 || s.nblocks > INT32_MAX / 2) return NW_ERR_ARG;
 
     int st;
@@ -288,8 +305,15 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
     // v_perm score tables when every substitution score minus 2*GAP fits int8
     // (the kernel falls back to compares on the device when s1 holds more than
     // kMaxPerm distinct characters).
-    const bool perm_ok = fits_i8(p->match - 2 * p->gap) && fits_i8(p->mismatch - 2 * p->gap) &&
+    const int32_t gw = sw ? 0 : p->gap;  // the w form's offset (NW only)
+    const bool perm_ok = fits_i8(p->match - 2 * gw) && fits_i8(p->mismatch - 2 * gw) &&
                          !(p->flags & NW_FLAG_NO_PROFILE);
+    if (sw) {
+        // per-strip best cells (zeroed on the launch stream) + best / key words
+        const size_t need = (size_t)(s.nstrips + 8) * sizeof(int32_t);
+        if ((st = grow((void **)&c->smax, &c->smax_cap, need)) != NW_OK) return st;
+        NW_HIP_TRY(hipMemsetAsync(c->smax, 0, (size_t)(s.nstrips + 8) * sizeof(int32_t), (hipStream_t)stream));
+    }
     if (nw::launch_rowpack(s1u, n1, s2u, n2, 0, perm_ok ? 1 : 0, c->meta, c->rowpack, qlen,
                            stream) != hipSuccess)
         return NW_ERR_HIP;
@@ -325,12 +349,24 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
     a.flags = p->flags;
     // s_memrealtime runs at 100 MHz: 100000 ticks per ms
     a.timeout_ticks = (uint64_t)(p->timeout_ms > 0 ? p->timeout_ms : 20000) * 100000ull;
+    a.sw = sw ? 1 : 0;
+    a.smax = sw ? c->smax : nullptr;
     if (nw::launch_fill(a, s.K, s.NC, (int)s.waves, stream) != hipSuccess) return NW_ERR_HIP;
     c->tagbase += (uint32_t)s.nstrips + 1u;
     c->last_waves = (int)s.waves;
     c->last_strips = (int)s.nstrips;
     c->last_sub = s.K;
     c->last_nc = s.NC;
+    c->last_col0 = (int)col0;
+    if (sw) {
+        // best cell: max over the strips, then the first row-major cell holding it
+        if (!c->swinfo) NW_HIP_TRY(hipMalloc(&c->swinfo, 16 * sizeof(int64_t)));
+        int32_t *best = c->smax + s.nstrips;
+        uint64_t *key = (uint64_t *)(c->swinfo + 8);
+        if (nw::launch_sw_locate(d_t, pitch, n1, n2, col0, (int32_t)(nw::kWave * s.K * s.NC), c->smax,
+                                 (int32_t)s.nstrips, key, best, stream) != hipSuccess)
+            return NW_ERR_HIP;
+    }
     return NW_OK;
 }
 
@@ -438,8 +474,94 @@ int nw_fill_device(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *d_s2
     out->substrips = c->last_sub;
     out->strip_waves = c->last_nc;
     int32_t score = 0;
-    NW_HIP_TRY(hipMemcpy(&score, d_t + n2 * pitch + n1, 4, hipMemcpyDeviceToHost));
+    if (p->mode == NW_MODE_SW) {
+        // best cell (nw_sw.hip locate): score and its first row-major position
+        uint64_t key = 0;
+        NW_HIP_TRY(hipMemcpy(&score, c->smax + c->last_strips, 4, hipMemcpyDeviceToHost));
+        NW_HIP_TRY(hipMemcpy(&key, c->swinfo + 8, 8, hipMemcpyDeviceToHost));
+        out->end_i = score > 0 ? (int64_t)(key >> 32) : 0;
+        out->end_j = score > 0 ? (int64_t)(key & 0xFFFFFFFFull) : 0;
+    } else {
+        NW_HIP_TRY(hipMemcpy(&score, d_t + n2 * pitch + n1, 4, hipMemcpyDeviceToHost));
+        out->end_i = n2;
+        out->end_j = n1;
+    }
     out->score = score;
+    return st;
+}
+
+int nw_sw_traceback(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *d_s2, int64_t n2,
+                    const nw_params *p, const int32_t *d_t, int64_t pitch, int64_t end_i, int64_t end_j,
+                    uint8_t *host_ops, int64_t ops_cap, nw_alignment *out) {
+    if (!c || !d_t || !p || !out || n1 < 0 || n2 < 0 || end_i < 0 || end_j < 0 || end_i > n2 || end_j > n1)
+        return NW_ERR_ARG;
+    if ((end_j > 0 && !d_s1) || (end_i > 0 && !d_s2) || (ops_cap > 0 && !host_ops) || ops_cap < 0)
+        return NW_ERR_ARG;
+    NW_HIP_TRY(hipSetDevice(c->device));
+    int st;
+    const size_t need = (size_t)std::max<int64_t>(end_i + end_j + 1, 1);
+    if ((st = grow((void **)&c->ops, &c->ops_cap, need)) != NW_OK) return st;
+    if (!c->swinfo) NW_HIP_TRY(hipMalloc(&c->swinfo, 16 * sizeof(int64_t)));
+    NW_HIP_TRY(hipEventRecord(c->ev0, nullptr));
+    if (nw::launch_sw_traceback(d_t, pitch, (const uint8_t *)d_s1, (const uint8_t *)d_s2, p->match, p->mismatch,
+                                p->gap, end_i, end_j, c->ops, (int64_t)need, c->swinfo, nullptr) != hipSuccess)
+        return NW_ERR_HIP;
+    NW_HIP_TRY(hipEventRecord(c->ev1, nullptr));
+    int64_t info[4];
+    NW_HIP_TRY(hipMemcpy(info, c->swinfo, sizeof info, hipMemcpyDeviceToHost));
+    float ms = 0.f;
+    NW_HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    std::memset(out, 0, sizeof *out);
+    out->end_i = end_i;
+    out->end_j = end_j;
+    out->n_ops = info[0];
+    out->begin_i = info[1];
+    out->begin_j = info[2];
+    out->traceback_ms = ms;
+    out->status = info[3] == 0 ? NW_OK : NW_ERR_HIP;
+    NW_HIP_TRY(hipMemcpy(&out->score, d_t + end_i * pitch + end_j, 4, hipMemcpyDeviceToHost));
+    if (info[3] != 0) return out->status;
+    if (info[0] > ops_cap) return NW_ERR_ARG;
+    if (info[0] > 0) {
+        // the kernel walks end -> begin; hand the ops over begin -> end
+        NW_HIP_TRY(hipMemcpy(host_ops, c->ops, (size_t)info[0], hipMemcpyDeviceToHost));
+        std::reverse(host_ops, host_ops + info[0]);
+    }
+    return NW_OK;
+}
+
+int nw_sw_align(const int8_t *s1, int64_t n1, const int8_t *s2, int64_t n2, const nw_params *p,
+                uint8_t *host_ops, int64_t ops_cap, nw_alignment *out) {
+    if (!p || p->mode != NW_MODE_SW || !out || n1 < 0 || n2 < 0 || (n1 > 0 && !s1) || (n2 > 0 && !s2))
+        return NW_ERR_ARG;
+    int dev = p->device;
+    if (dev < 0 && hipGetDevice(&dev) != hipSuccess) return NW_ERR_NODEVICE;
+    nw_ctx *c = nullptr;
+    int st = nw_ctx_create(dev, &c);
+    if (st != NW_OK) return st;
+    const int64_t pitch = nw_table_pitch(n1);
+    int32_t *d_alloc = nullptr;
+    int8_t *d_s1 = nullptr, *d_s2 = nullptr;
+    if (hipMalloc(&d_alloc, (size_t)nw_table_bytes(n1, n2) + 256) != hipSuccess ||
+        hipMalloc(&d_s1, (size_t)std::max<int64_t>(n1, 1)) != hipSuccess ||
+        hipMalloc(&d_s2, (size_t)std::max<int64_t>(n2, 1)) != hipSuccess)
+        st = NW_ERR_OOM;
+    int32_t *d_t = d_alloc ? d_alloc + (n1 >= 1 ? nw_table_offset() : 0) : nullptr;
+    if (st == NW_OK && n1 > 0 && hipMemcpy(d_s1, s1, (size_t)n1, hipMemcpyHostToDevice) != hipSuccess)
+        st = NW_ERR_HIP;
+    if (st == NW_OK && n2 > 0 && hipMemcpy(d_s2, s2, (size_t)n2, hipMemcpyHostToDevice) != hipSuccess)
+        st = NW_ERR_HIP;
+    nw_result r;
+    std::memset(&r, 0, sizeof r);
+    if (st == NW_OK) st = nw_fill_device(c, d_s1, n1, d_s2, n2, p, d_t, pitch, nullptr, &r);
+    if (st == NW_OK) st = nw_sw_traceback(c, d_s1, n1, d_s2, n2, p, d_t, pitch, r.end_i, r.end_j, host_ops,
+                                          ops_cap, out);
+    if (st == NW_OK) out->fill_ms = r.kernel_ms;
+    if (d_alloc) (void)hipFree(d_alloc);
+    if (d_s1) (void)hipFree(d_s1);
+    if (d_s2) (void)hipFree(d_s2);
+    nw_ctx_destroy(c);
+    out->status = st;
     return st;
 }
 
@@ -493,6 +615,58 @@ int nw_fill(const int8_t *s1, int64_t n1, const int8_t *s2, int64_t n2, const nw
     (void)hipFree(d_alloc);
     if (d_s1) (void)hipFree(d_s1);
     if (d_s2) (void)hipFree(d_s2);
+    r.status = st;
+    if (out) *out = r;
+    return st;
+}
+
+int nw_fill_emb(const int8_t *s1, int64_t n1, const int8_t *s2, int64_t n2, const nw_params *p,
+                int32_t *host_t, nw_result *out) {
+    // The emb layout of src/idxarray/idxarray-emb-mt.cpp:7-37 / src/common/driver2.cpp:20-22:
+    // nCols = n1 + 2; column 0 holds each row's progress counter, which the reference
+    // fill leaves at its final value nCols (:49, the row loop's `int& j`, and :36 for
+    // row 0); columns 1 .. n1+1 hold the serial table.  Fill as nw_fill, copy the
+    // table into columns 1.., then write column 0.
+    nw_params def;
+    if (!p) {
+        nw_params_default(&def);
+        p = &def;
+    }
+    if (!host_t || n1 < 0 || n2 < 0 || (n1 > 0 && !s1) || (n2 > 0 && !s2)) return NW_ERR_ARG;
+    nw_result r;
+    std::memset(&r, 0, sizeof r);
+    int st = NW_OK;
+    {
+        // nw_fill with the table landing in columns 1 .. n1+1 of rows of n1+2
+        int dev = p->device;
+        if (dev < 0 && hipGetDevice(&dev) != hipSuccess) return NW_ERR_NODEVICE;
+        nw_ctx *c = nullptr;
+        if ((st = nw_ctx_create(dev, &c)) != NW_OK) return st;
+        const int64_t pitch = nw_table_pitch(n1);
+        int32_t *d_alloc = nullptr;
+        int8_t *d_s1 = nullptr, *d_s2 = nullptr;
+        if (hipMalloc(&d_alloc, (size_t)nw_table_bytes(n1, n2) + 256) != hipSuccess ||
+            hipMalloc(&d_s1, (size_t)std::max<int64_t>(n1, 1)) != hipSuccess ||
+            hipMalloc(&d_s2, (size_t)std::max<int64_t>(n2, 1)) != hipSuccess)
+            st = NW_ERR_OOM;
+        int32_t *d_t = d_alloc ? d_alloc + (n1 >= 1 ? nw_table_offset() : 0) : nullptr;
+        if (st == NW_OK && n1 > 0 && hipMemcpy(d_s1, s1, (size_t)n1, hipMemcpyHostToDevice) != hipSuccess)
+            st = NW_ERR_HIP;
+        if (st == NW_OK && n2 > 0 && hipMemcpy(d_s2, s2, (size_t)n2, hipMemcpyHostToDevice) != hipSuccess)
+            st = NW_ERR_HIP;
+        if (st == NW_OK) st = nw_fill_device(c, d_s1, n1, d_s2, n2, p, d_t, pitch, nullptr, &r);
+        const size_t w = (size_t)(n1 + 1) * sizeof(int32_t);
+        if (st == NW_OK && hipMemcpy2D(host_t + 1, (size_t)(n1 + 2) * sizeof(int32_t), d_t,
+                                       (size_t)pitch * 4, w, (size_t)(n2 + 1),
+                                       hipMemcpyDeviceToHost) != hipSuccess)
+            st = NW_ERR_HIP;
+        if (d_alloc) (void)hipFree(d_alloc);
+        if (d_s1) (void)hipFree(d_s1);
+        if (d_s2) (void)hipFree(d_s2);
+        nw_ctx_destroy(c);
+    }
+    if (st == NW_OK)
+        for (int64_t i = 0; i <= n2; ++i) host_t[i * (n1 + 2)] = (int32_t)(n1 + 2);
     r.status = st;
     if (out) *out = r;
     return st;

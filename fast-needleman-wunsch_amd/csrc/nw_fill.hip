@@ -308,13 +308,19 @@ __device__ __forceinline__ void static_for(F &&f) {
 // The compare forms test raw byte equality, the reference's match test
 // (serial.cpp:23-24); ms' / mm' / the table bytes have 2*GAP pre-subtracted
 // because the cells hold w = t - GAP*(i+j).
-enum Sub { SUB_PERM = 0, SUB_UNIT = 1, SUB_GEN = 2 };
+//   SUB_PERM_SW / SUB_GEN_SW : Smith-Waterman (local alignment, BASELINE config 5):
+//              the cells hold t itself (plain form: the 0 floor is not constant
+//              in the w form) and  t = max(0, diag + s, max(up, left) + GAP)
+//              (v_max_i32, v_add, v_max3 after the diag add); the substitution
+//              as SUB_PERM / SUB_GEN without the 2*GAP.
+enum Sub { SUB_PERM = 0, SUB_UNIT = 1, SUB_GEN = 2, SUB_PERM_SW = 3, SUB_GEN_SW = 4 };
+template <int MODE> constexpr bool is_sw() { return MODE == SUB_PERM_SW || MODE == SUB_GEN_SW; }
 
 template <int QB, int KB, int MODE>
 __device__ __forceinline__ int32_t diag_plus_sub(uint32_t w, uint32_t apk, int32_t diag,
                                                  int32_t msp, int32_t mmp) {
     int32_t d;
-    if constexpr (MODE == SUB_PERM) {
+    if constexpr (MODE == SUB_PERM || MODE == SUB_PERM_SW) {
         // w = v_perm result: byte QB = s'(a_k, row of step QB)
         asm("v_add_u32_sdwa %0, %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD "
             "src0_sel:DWORD src1_sel:BYTE_%c3"
@@ -473,7 +479,7 @@ __device__ __forceinline__ void run_iter(char *__restrict__ lds, int it, const u
         if constexpr (g + 1 < 16) fq = feed4[g + 1];
         const uint32_t word = pk[g >> 2][g & 3];  // row characters of steps 4g .. 4g+3
         uint32_t sc[C];
-        if constexpr (MODE == SUB_PERM) {
+        if constexpr (MODE == SUB_PERM || MODE == SUB_PERM_SW) {
 #pragma unroll
             for (int k = 0; k < C; ++k) sc[k] = __builtin_amdgcn_perm(S.thi[k], S.tlo[k], word);
         }
@@ -495,10 +501,16 @@ __device__ __forceinline__ void run_iter(char *__restrict__ lds, int it, const u
             (void)tv;
             static_for<0, C>([&](auto kc) {
                 constexpr int k = decltype(kc)::value;
-                const uint32_t w = MODE == SUB_PERM ? sc[k] : word;
+                const uint32_t w = (MODE == SUB_PERM || MODE == SUB_PERM_SW) ? sc[k] : word;
                 const int32_t d = diag_plus_sub<q, k, MODE>(w, S.apk, diag, msp, mmp);
-                // w = max(w_diag + s - 2 GAP, w_up, w_left)  (w = t - GAP*(i+j))
-                int32_t x = max(max(d, S.u[k]), left);
+                int32_t x;
+                if constexpr (is_sw<MODE>()) {
+                    // t = max(0, t_diag + s, max(t_up, t_left) + GAP)
+                    x = max(max(d, max(S.u[k], left) + gap), 0);
+                } else {
+                    // w = max(w_diag + s - 2 GAP, w_up, w_left)  (w = t - GAP*(i+j))
+                    x = max(max(d, S.u[k]), left);
+                }
                 diag = S.u[k];
                 // lanes still above row 1 hold row 0 (the top boundary / halo)
                 if constexpr (RAMP) x = act ? x : S.u[k];
@@ -552,8 +564,11 @@ template <int C, int NC, int MODE>
 __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restrict__ lds, int p,
                                               int j, int lane) {
     typedef Lay<C, NC> L;
+    constexpr bool SW = is_sw<MODE>();
     const int32_t gap = A.gap;
-    const int32_t msp = A.match - 2 * gap, mmp = A.mismatch - 2 * gap;
+    // the w form (NW) subtracts GAP*(i+j) from every cell; SW cells are plain
+    const int32_t gw = SW ? 0 : gap;
+    const int32_t msp = A.match - 2 * gw, mmp = A.mismatch - 2 * gw;
     const int64_t c0 = A.col0 + (int64_t)p * (NC * 64 * C) + (int64_t)j * (64 * C);
     const int64_t cl = c0 + (int64_t)C * lane;  // first column of this lane
     int32_t *ctr = (int32_t *)(lds + L::kCtl) + j * L::kCtlWords;
@@ -567,7 +582,7 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
     int32_t top[C];
     int32_t bnd0 = 0;
 #pragma unroll
-    for (int k = 0; k < C; ++k) top[k] = (int32_t)((cl + k) * (int64_t)gap);
+    for (int k = 0; k < C; ++k) top[k] = (int32_t)((cl + k) * (int64_t)gw);  // SW: row 0 is 0
     if (A.halo_in != nullptr) {
         const uint64_t h0 = __builtin_amdgcn_s_memrealtime();
         for (;;) {
@@ -606,8 +621,8 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
         const int64_t c = cl + k;
         const uint32_t a = (c >= 1 && c <= A.n1) ? (uint32_t)A.s1[c - 1] : 0u;
         S.apk |= a << (8 * k);
-        S.u[k] = top[k] - (int32_t)((cl + k) * (int64_t)gap);  // w[0][c] = t[0][c] - GAP*c
-        if constexpr (MODE == SUB_PERM) {
+        S.u[k] = top[k] - (int32_t)((cl + k) * (int64_t)gw);  // w[0][c] = t[0][c] - GAP*c
+        if constexpr (MODE == SUB_PERM || MODE == SUB_PERM_SW) {
             const uint32_t x = (c >= 1 && c <= A.n1) ? (uint32_t)A.charmap[a] : 0xFFu;
             const uint32_t msb = (uint32_t)msp & 255u;
             const uint32_t sh = 8u * (x & 3u), keep = ~(255u << sh), put = msb << sh;
@@ -802,6 +817,14 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
     }
 }
 
+// Smith-Waterman: fold a store wave's running maximum into the strip's word
+// A.smax[p] (zeroed before the launch; the locate kernel reads them).
+__device__ __forceinline__ void strip_max(const FillArgs &A, int p, int32_t vmax) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) vmax = max(vmax, __shfl_xor(vmax, off));
+    if ((threadIdx.x & 63) == 0) atomicMax(A.smax + p, vmax);
+}
+
 // Store wave q of compute wave j on strip p: rows 0 .. n2 of ring j leave as
 // whole row segments.  One 16-byte-per-lane store covers NR = 4/C rows (1 KB:
 // a row of a C = 4 ring, two rows of a C = 2 ring): lane l takes row
@@ -837,11 +860,18 @@ __device__ __forceinline__ void store_strip(const FillArgs &A, char *__restrict_
     char *scr = (char *)(A.scratch + (int64_t)blockIdx.x * kScratchWords);
     const int32_t f0 = q * BATCH;
     // the ring holds w = t - GAP*(r + c) (run_iter): kc[e] = GAP*(r + c) of element
-    // e of this lane's piece in its current batch (wrapping int32, like the cells)
-    const uint32_t ug = (uint32_t)A.gap;
+    // e of this lane's piece in its current batch (wrapping int32, like the cells);
+    // Smith-Waterman rings hold t itself (ug = 0)
+    const uint32_t ug = A.sw ? 0u : (uint32_t)A.gap;
     uint32_t kc[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) kc[e] = ug * (uint32_t)(f0 + ro) + ug * (uint32_t)(c0 + 4 * cq + e);
+    // SW: running maximum of this lane's cells (columns <= n1 only) for the
+    // strip's best-cell word A.smax[p]
+    uint32_t cval = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) cval |= (c0 + 4 * cq + e <= A.n1 ? 1u : 0u) << e;
+    int32_t vmax = 0;
     char *rowp = timing ? scr : (char *)(A.table + c0) + (int64_t)f0 * rowb;
     const uint32_t voff = (uint32_t)(ro * rowb) + (uint32_t)cq * 16u;
     // col0 = 1: strip 0's first ring also stores the boundary column 0,
@@ -898,6 +928,15 @@ __device__ __forceinline__ void store_strip(const FillArgs &A, char *__restrict_
         // (in-order LDS: the counter is written after the reads have read)
         lds_order();
         ctr_store(mine, f + NS * BATCH);
+        if (A.sw) {
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {
+                const bool rok = f + g * NR + ro < nrows;
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    vmax = max(vmax, (rok && ((cval >> e) & 1u)) ? (int32_t)v[g][e] : 0);
+            }
+        }
         if (want - f == BATCH) {
 #pragma unroll
             for (int g = 0; g < NG; ++g)
@@ -913,12 +952,13 @@ __device__ __forceinline__ void store_strip(const FillArgs &A, char *__restrict_
             for (int g = 0; g < NG; ++g) {
                 const int32_t r = f + g * NR + ro;
                 if (cq == 0 && r < nrows)
-                    *(int32_t *)(rowp + (int64_t)g * NR * rowb + (int64_t)voff - 4) = bnd0 + r * A.gap;
+                    *(int32_t *)(rowp + (int64_t)g * NR * rowb + (int64_t)voff - 4) = bnd0 + r * (int32_t)ug;
             }
         }
         rowp += NS * BATCH * rowb;
     }
     ctr_store(mine, kDone);
+    if (A.sw) strip_max(A, p, vmax);
     // Row band: hand this ring's columns of the last row (n2) to the next band.
     // The table stores are plain (write-back L2), so: drain them, write the XCD's
     // L2 back (agent release), re-read the row with sc1 loads, publish
@@ -969,7 +1009,7 @@ __device__ __forceinline__ void store_strip_grp(const FillArgs &A, char *__restr
     const int64_t rowb = timing ? 0 : A.pitch * 4;
     char *scr = (char *)(A.scratch + (int64_t)blockIdx.x * kScratchWords);
     const int32_t f0 = q * BATCH;
-    const uint32_t ug = (uint32_t)A.gap;
+    const uint32_t ug = A.sw ? 0u : (uint32_t)A.gap;  // SW rings hold t itself
     // ring byte offset (within the ring) of column a = 32h + 4cq + k of row f0 + ro,
     // and kc = GAP * (row + column) of it (the ring holds w = t - GAP*(i+j))
     uint32_t pa[2][4], kc[2][4];
@@ -986,6 +1026,13 @@ __device__ __forceinline__ void store_strip_grp(const FillArgs &A, char *__restr
     bool col_ok[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) col_ok[h] = c0 + 32 * h + 4 * cq + 4 <= A.pitch;
+    // SW: running maximum of this lane's cells (columns <= n1) for A.smax[p]
+    uint32_t cval = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) cval |= (c0 + 32 * h + 4 * cq + k <= A.n1 ? 1u : 0u) << (4 * h + k);
+    int32_t vmax = 0;
     char *rowp = timing ? scr : (char *)(A.table + c0) + (int64_t)f0 * rowb;
     const uint32_t voff = (uint32_t)(ro * rowb) + (uint32_t)cq * 16u;
     const bool bcol = A.col0 != 0 && p == 0 && j == 0 && !timing;
@@ -1038,6 +1085,17 @@ __device__ __forceinline__ void store_strip_grp(const FillArgs &A, char *__restr
         // (in-order LDS: this counter store executes after the batch's reads)
         lds_order();
         ctr_store(mine, f + NS * BATCH);
+        if (A.sw) {
+#pragma unroll
+            for (int g = 0; g < NU; ++g) {
+                const bool rok = f + g * 8 + ro < nrows;
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        vmax = max(vmax, (rok && ((cval >> (4 * h + k)) & 1u)) ? (int32_t)v[g][h][k] : 0);
+            }
+        }
         const uint64_t t0 = trace ? __builtin_amdgcn_s_memtime() : 0;
         char *rp = rowp + (int64_t)(f - f0) * rowb;
         if (min(f + BATCH, nrows) - f == BATCH) {
@@ -1059,7 +1117,7 @@ __device__ __forceinline__ void store_strip_grp(const FillArgs &A, char *__restr
             for (int g = 0; g < NU; ++g) {
                 const int32_t r = f + g * 8 + ro;
                 if (cq == 0 && r < nrows)
-                    *(int32_t *)(rp + (int64_t)g * 8 * rowb + (int64_t)voff - 4) = bnd0 + r * A.gap;
+                    *(int32_t *)(rp + (int64_t)g * 8 * rowb + (int64_t)voff - 4) = bnd0 + r * (int32_t)ug;
             }
         }
         if (trace) ts += __builtin_amdgcn_s_memtime() - t0;
@@ -1100,6 +1158,7 @@ __device__ __forceinline__ void store_strip_grp(const FillArgs &A, char *__restr
         }
     }
     ctr_store(mine, kDone);
+    if (A.sw) strip_max(A, p, vmax);
     if (trace && lane == 0) {
         uint64_t *trw = A.trace + (int64_t)p * kTraceWords;
         trw[16] = tw;
@@ -1122,6 +1181,12 @@ __device__ __forceinline__ void store_strip_grp(const FillArgs &A, char *__restr
                                ((uint64_t)A.halo_tag << 32) | (uint32_t)(bnd0 + (int32_t)A.n2 * A.gap),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+}
+
+// Strip shapes built with the Smith-Waterman modes (the tuned ones; the others
+// refuse SW launches in nw_capi.cpp) -- each mode is a full copy of the loop.
+constexpr bool sw_shape(int c, int nc) {
+    return (c == 2 && nc == 2) || (c == 1 && nc == 4) || (c == 4 && nc == 1) || (c == 2 && nc == 1);
 }
 
 // Persistent grid of workgroups of NC compute waves (0 .. NC-1) and NC*kSPR
@@ -1148,12 +1213,24 @@ __global__ __launch_bounds__((64 * Lay<C, NC>::kWaves)) void nw_fill_strips(Fill
             // table form when the launch allows it (scores fit int8) and s1 has
             // at most kMaxPerm distinct characters (nw_charmap), else compares
             const uint32_t np = __builtin_amdgcn_readfirstlane(ctrl_load(A.nprof));
-            if (A.perm != 0 && np <= kMaxPerm)
+            bool sw_done = false;
+            if constexpr (sw_shape(C, NC) && !UNIT) {  // (SW launches use the generic kernel)
+                if (A.sw) {
+                    if (A.perm != 0 && np <= kMaxPerm)
+                        compute_strip<C, NC, SUB_PERM_SW>(A, lds, p, wave, lane);
+                    else
+                        compute_strip<C, NC, SUB_GEN_SW>(A, lds, p, wave, lane);
+                    sw_done = true;
+                }
+            }
+            if (sw_done) {
+            } else if (A.perm != 0 && np <= kMaxPerm) {
                 compute_strip<C, NC, SUB_PERM>(A, lds, p, wave, lane);
-            else if (UNIT)
+            } else if (UNIT) {
                 compute_strip<C, NC, SUB_UNIT>(A, lds, p, wave, lane);
-            else
+            } else {
                 compute_strip<C, NC, SUB_GEN>(A, lds, p, wave, lane);
+            }
         } else {
             const int b = wave - NC;
             if constexpr (L::kGrp)
@@ -1244,7 +1321,7 @@ int launch_rowpack(const uint8_t *d_s1, int64_t n1, const uint8_t *d_s2, int64_t
 template <int C, int NC>
 static void launch_c(const FillArgs &a, int grid, hipStream_t s) {
     const dim3 block(64 * Lay<C, NC>::kWaves);
-    if (a.match - a.mismatch == 1)
+    if (a.match - a.mismatch == 1 && !a.sw)
         hipLaunchKernelGGL((nw_fill_strips<C, NC, true>), dim3(grid), block, 0, s, a);
     else
         hipLaunchKernelGGL((nw_fill_strips<C, NC, false>), dim3(grid), block, 0, s, a);
@@ -1270,6 +1347,10 @@ bool shape_ok(int substrips, int strip_waves) {
         default:
             return false;
     }
+}
+
+bool sw_shape_ok(int substrips, int strip_waves) {
+    return shape_ok(substrips, strip_waves) && sw_shape(substrips, strip_waves);
 }
 
 int launch_fill(const FillArgs &a, int substrips, int strip_waves, int grid, void *stream) {

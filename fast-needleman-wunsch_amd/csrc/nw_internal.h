@@ -50,7 +50,24 @@ struct FillArgs {
     int32_t match, mismatch, gap;
     int32_t flags;             // debug: bit0 = send table stores to the scratch tile (timing only)
     uint64_t timeout_ticks;    // bound of every in-kernel wait (s_memrealtime ticks, 100 MHz)
+    // Smith-Waterman (local alignment): cells t = max(0, ...), row/column 0 = 0;
+    // store waves fold each strip's best cell into smax[p] (zeroed before launch)
+    int32_t sw;
+    int32_t *smax;
 };
+bool sw_shape_ok(int substrips, int strip_waves);
+// best cell of an SW table: reduce smax[nstrips] and find the first row-major cell
+// holding the maximum (out8[0] = score, out8[1..2] = row, out8[3..4] = column as
+// 64-bit halves); device buffers, asynchronous on `stream`
+int launch_sw_locate(const int32_t *table, int64_t pitch, int64_t n1, int64_t n2, int64_t col0,
+                     int32_t strip_cols, const int32_t *smax, int32_t nstrips, uint64_t *key, int32_t *best,
+                     void *stream);
+// traceback from (end_i, end_j) (see nw_fill.hip nw_sw_traceback); ops[] gets one
+// byte per step from the end cell back (0 diag, 1 up, 2 left), info8[0] = steps,
+// [1] = begin row, [2] = begin column, [3] = status (0 ok, 1 ops buffer too small)
+int launch_sw_traceback(const int32_t *table, int64_t pitch, const uint8_t *s1, const uint8_t *s2,
+                        int32_t match, int32_t mismatch, int32_t gap, int64_t end_i, int64_t end_j,
+                        uint8_t *ops, int64_t ops_cap, int64_t *info, void *stream);
 
 // Launch helpers implemented in nw_fill.hip.  Return hipError_t as int.
 // charmap of s1 into meta, then the row packs (mapped when perm allows it)

@@ -22,6 +22,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NWHIP_LIB") or os.path.join(HERE, "build", "libnwhip.so")
 
 NW_OK, NW_ERR_ARG, NW_ERR_HIP, NW_ERR_OOM, NW_ERR_TIMEOUT, NW_ERR_NODEVICE, NW_ERR_UNSUPPORTED = range(7)
+MODE_NW, MODE_SW = 0, 1  # nw_params.mode: global (the reference fills) / Smith-Waterman local
 
 # every symbol include/nw_hip.h declares (checked by tests/test_host.py)
 EXPORTS = ["nw_params_default", "nw_strerror", "nw_version", "nw_fill", "nw_table_pitch",
@@ -29,7 +30,7 @@ EXPORTS = ["nw_params_default", "nw_strerror", "nw_version", "nw_fill", "nw_tabl
            "nw_fill_device", "nw_fill_device_async", "nw_ctx_status", "nw_read_bdna", "nw_free",
            "nw_synth_bdna", "nw_band_layout", "nw_halo_bytes", "nw_fill_band_async",
            "nw_ipc_get_handle", "nw_ipc_open_handle", "nw_ipc_close_handle", "nw_halo_alloc",
-           "nw_halo_free", "nw_tuned_shape", "nw_debug_ctrl", "nw_debug_set_trace",
+           "nw_halo_free", "nw_fill_emb", "nw_sw_align", "nw_sw_traceback", "nw_tuned_shape", "nw_debug_ctrl", "nw_debug_set_trace",
            "nw_debug_trace_words"]
 IPC_HANDLE_BYTES = 64
 
@@ -45,7 +46,15 @@ class NwResult(ctypes.Structure):
     _fields_ = [("score", ctypes.c_int32), ("status", ctypes.c_int32), ("cells", ctypes.c_int64),
                 ("kernel_ms", ctypes.c_double), ("table_bytes", ctypes.c_double),
                 ("strips", ctypes.c_int32), ("waves", ctypes.c_int32),
-                ("substrips", ctypes.c_int32), ("strip_waves", ctypes.c_int32)]
+                ("substrips", ctypes.c_int32), ("strip_waves", ctypes.c_int32),
+                ("end_i", ctypes.c_int64), ("end_j", ctypes.c_int64)]
+
+
+class NwAlignment(ctypes.Structure):
+    """nw_alignment (include/nw_hip.h): a Smith-Waterman alignment."""
+    _fields_ = [("score", ctypes.c_int32), ("status", ctypes.c_int32), ("begin_i", ctypes.c_int64),
+                ("begin_j", ctypes.c_int64), ("end_i", ctypes.c_int64), ("end_j", ctypes.c_int64),
+                ("n_ops", ctypes.c_int64), ("fill_ms", ctypes.c_double), ("traceback_ms", ctypes.c_double)]
 
 
 class NwBand(ctypes.Structure):
@@ -89,6 +98,14 @@ def lib() -> ctypes.CDLL:
     L.nw_version.restype = ctypes.c_char_p
     L.nw_fill.argtypes = [_i8p, ctypes.c_int64, _i8p, ctypes.c_int64, ctypes.POINTER(NwParams),
                           _i32p, ctypes.POINTER(NwResult)]
+    L.nw_fill_emb.argtypes = L.nw_fill.argtypes
+    _u8p = ctypes.POINTER(ctypes.c_uint8)
+    L.nw_sw_align.argtypes = [_i8p, ctypes.c_int64, _i8p, ctypes.c_int64, ctypes.POINTER(NwParams), _u8p,
+                              ctypes.c_int64, ctypes.POINTER(NwAlignment)]
+    L.nw_sw_traceback.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                  ctypes.c_int64, ctypes.POINTER(NwParams), ctypes.c_void_p, ctypes.c_int64,
+                                  ctypes.c_int64, ctypes.c_int64, _u8p, ctypes.c_int64,
+                                  ctypes.POINTER(NwAlignment)]
     L.nw_table_pitch.argtypes = [ctypes.c_int64]
     L.nw_table_pitch.restype = ctypes.c_int64
     L.nw_table_bytes.argtypes = [ctypes.c_int64, ctypes.c_int64]
@@ -157,7 +174,7 @@ class Scheme:
 
 
 def params(scheme=(1, 0, -1), waves: int = 0, device: int = -1, flags: int = 0,
-           substrips: int = 0, strip_waves: int = 0, timeout_ms: int = 0) -> NwParams:
+           substrips: int = 0, strip_waves: int = 0, timeout_ms: int = 0, mode: int = MODE_NW) -> NwParams:
     if isinstance(scheme, Scheme):
         scheme = (scheme.match, scheme.mismatch, scheme.gap)
     p = NwParams()
@@ -169,7 +186,22 @@ def params(scheme=(1, 0, -1), waves: int = 0, device: int = -1, flags: int = 0,
     p.substrips = int(substrips)
     p.strip_waves = int(strip_waves)
     p.timeout_ms = int(timeout_ms)
+    p.mode = int(mode)
     return p
+
+
+def sw_align(s1, s2, scheme=(1, -1, -1), device: int = -1, substrips: int = 0, strip_waves: int = 0):
+    """Smith-Waterman local alignment on the device (nw_sw_align): returns
+    (NwAlignment, ops) with ops a uint8 array in path order (0 diag, 1 up, 2 left)."""
+    a, b = _seq(s1), _seq(s2)
+    ops = np.empty(a.size + b.size + 1, dtype=np.uint8)
+    out = NwAlignment()
+    p = params(scheme, device=device, substrips=substrips, strip_waves=strip_waves, mode=MODE_SW)
+    st = lib().nw_sw_align(a.ctypes.data_as(_i8p), a.size, b.ctypes.data_as(_i8p), b.size, ctypes.byref(p),
+                           ops.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), ops.size, ctypes.byref(out))
+    if st != NW_OK:
+        raise NwError(st, "nw_sw_align")
+    return out, ops[:out.n_ops].copy()
 
 
 def _seq(s) -> np.ndarray:
@@ -365,7 +397,7 @@ class Context:
 
     def fill(self, d_s1, d_s2, table, scheme=(1, 0, -1), waves: int = 0, stream=None,
              sync: bool = True, flags: int = 0, substrips: int = 0, strip_waves: int = 0,
-             timeout_ms: int = 0):
+             timeout_ms: int = 0, mode: int = MODE_NW):
         """d_s1/d_s2: int8/uint8 CUDA tensors; table: from alloc_table.  Returns NwResult
         when sync, else None (launch only)."""
         import torch
@@ -375,7 +407,7 @@ class Context:
         if stream is None:
             stream = torch.cuda.current_stream(table.device)
         sp = ctypes.c_void_p(stream.cuda_stream)
-        p = params(scheme, waves, self.device, flags, substrips, strip_waves, timeout_ms)
+        p = params(scheme, waves, self.device, flags, substrips, strip_waves, timeout_ms, mode)
         args = (self._h, ctypes.c_void_p(d_s1.data_ptr() if n1 else 0), n1,
                 ctypes.c_void_p(d_s2.data_ptr() if n2 else 0), n2, ctypes.byref(p),
                 ctypes.c_void_p(table.data_ptr()), table.shape[1], sp)
@@ -422,6 +454,22 @@ class Context:
                                       ctypes.c_void_p(stream.cuda_stream))
         if st != NW_OK:
             raise NwError(st, "nw_fill_band_async")
+
+    def sw_traceback(self, d_s1, d_s2, table, end, scheme=(1, -1, -1)):
+        """Traceback of a device SW table (filled with mode=MODE_SW) from end = (i, j):
+        (NwAlignment, ops) as sw_align."""
+        n1, n2 = int(d_s1.numel()), int(d_s2.numel())
+        ops = np.empty(end[0] + end[1] + 1, dtype=np.uint8)
+        out = NwAlignment()
+        p = params(scheme, device=self.device, mode=MODE_SW)
+        st = lib().nw_sw_traceback(self._h, ctypes.c_void_p(d_s1.data_ptr() if n1 else 0), n1,
+                                   ctypes.c_void_p(d_s2.data_ptr() if n2 else 0), n2, ctypes.byref(p),
+                                   ctypes.c_void_p(table.data_ptr()), table.shape[1], int(end[0]), int(end[1]),
+                                   ops.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), ops.size,
+                                   ctypes.byref(out))
+        if st != NW_OK:
+            raise NwError(st, "nw_sw_traceback")
+        return out, ops[:out.n_ops].copy()
 
     def set_trace(self, trace_tensor) -> None:
         """Debug: per-strip timeline (start, end, waits, ...: tools/trace_strips.py) into

@@ -41,7 +41,10 @@ enum {
     NW_ERR_UNSUPPORTED = 6
 };
 
-enum { NW_MODE_NW = 0 };
+/* nw_params.mode: global alignment (the reference fills) or Smith-Waterman local
+ * alignment (BASELINE config 5; no reference counterpart -- conventions in
+ * nw_sw_align below) */
+enum { NW_MODE_NW = 0, NW_MODE_SW = 1 };
 
 /* nw_params.flags (0 = normal fill) */
 enum {
@@ -80,7 +83,19 @@ typedef struct nw_result {
     int32_t waves;          /* persistent workers launched                */
     int32_t substrips;      /* columns per lane of a compute wave         */
     int32_t strip_waves;    /* compute waves per strip                    */
+    int64_t end_i, end_j;   /* cell `score` was read from: (n2, n1) for NW; for SW
+                               the best cell, first in row-major order     */
 } nw_result;
+
+/* A Smith-Waterman alignment (nw_sw_align / nw_sw_traceback). */
+typedef struct nw_alignment {
+    int32_t score;           /* t[end_i][end_j], the table maximum            */
+    int32_t status;
+    int64_t begin_i, begin_j; /* cell where the traceback reached t == 0      */
+    int64_t end_i, end_j;    /* best cell (first row-major maximum)          */
+    int64_t n_ops;           /* ops written, path order begin -> end          */
+    double fill_ms, traceback_ms;
+} nw_alignment;
 
 /* Fill `p` with the reference defaults (1, 0, -1). */
 void nw_params_default(nw_params *p);
@@ -101,6 +116,30 @@ const char *nw_version(void);
  */
 int nw_fill(const int8_t *s1, int64_t n1, const int8_t *s2, int64_t n2,
             const nw_params *p, int32_t *host_t, nw_result *out);
+
+/*
+ * The same fill into the "emb" table layout of the reference's second driver
+ * (src/common/driver2.cpp:20-22 allocates (s1.size+2) * (s2.size+1) ints;
+ * src/idxarray/idxarray-emb-mt.cpp:4-65 fills it): rows of n1+2 ints, column 0
+ * = each row's progress counter at its final value n1+2, columns 1 .. n1+1 = the
+ * serial table.  host_t is required.
+ */
+int nw_fill_emb(const int8_t *s1, int64_t n1, const int8_t *s2, int64_t n2,
+                const nw_params *p, int32_t *host_t, nw_result *out);
+
+/*
+ * Smith-Waterman local alignment with on-device traceback (BASELINE config 5).
+ * Table: t[i][0] = t[0][j] = 0, t[i][j] = max(0, t[i-1][j-1] + s, t[i-1][j] + GAP,
+ * t[i][j-1] + GAP) (gap <= 0).  Best cell: the maximum, first in row-major
+ * order.  Traceback from it while t > 0, preferring diag > up > left (the order
+ * of serial.cpp:24-30's max).  ops[k] (path order, begin -> end): 0 = diagonal
+ * (s1[j-1] against s2[i-1]), 1 = up (s2[i-1] against a gap), 2 = left (s1[j-1]
+ * against a gap); ops_cap >= n1 + n2 always suffices.  p->mode must be
+ * NW_MODE_SW.  The reference has no local alignment: parity is against the
+ * build's CPU restatement (oracle/nw_oracle.c), not the reference.
+ */
+int nw_sw_align(const int8_t *s1, int64_t n1, const int8_t *s2, int64_t n2, const nw_params *p,
+                uint8_t *ops, int64_t ops_cap, nw_alignment *out);
 
 /* Device-resident API ------------------------------------------------------ */
 typedef struct nw_ctx nw_ctx;
@@ -153,6 +192,13 @@ int64_t nw_ctx_workspace_bytes(int64_t n1, int64_t n2, int32_t waves);
 int nw_fill_device(nw_ctx *ctx, const int8_t *d_s1, int64_t n1,
                    const int8_t *d_s2, int64_t n2, const nw_params *p,
                    int32_t *d_t, int64_t pitch, void *stream, nw_result *out);
+
+/* Traceback of a device-resident SW table filled by nw_fill_device (mode SW)
+ * from (end_i, end_j) (nw_result.end_i/end_j); ops copied to the host as in
+ * nw_sw_align. */
+int nw_sw_traceback(nw_ctx *ctx, const int8_t *d_s1, int64_t n1, const int8_t *d_s2, int64_t n2,
+                    const nw_params *p, const int32_t *d_t, int64_t pitch, int64_t end_i, int64_t end_j,
+                    uint8_t *ops, int64_t ops_cap, nw_alignment *out);
 
 /* Launch-only variant for timing loops: no synchronisation, no readback. */
 int nw_fill_device_async(nw_ctx *ctx, const int8_t *d_s1, int64_t n1,

@@ -238,3 +238,93 @@ void nw_oracle_synth(uint64_t seed, int64_t n, int8_t *out) {
         out[i] = (int8_t)(1 + (z >> 62));
     }
 }
+
+/*
+ * Smith-Waterman (local alignment, BASELINE config 5).  The reference has NO
+ * local alignment (README.md:2 states the intent only), so this restatement
+ * defines the semantics the GPU path is checked against -- "parity unpinned":
+ *   t[i][0] = t[0][j] = 0;
+ *   t[i][j] = max(0, t[i-1][j-1] + s(s1[j-1], s2[i-1]), t[i-1][j] + GAP, t[i][j-1] + GAP)
+ *   (the recurrence of serial.cpp:21-33 with a 0 floor; s as serial.cpp:23-24);
+ *   best cell = the maximum, first in row-major order;
+ *   traceback from it while t > 0, preferring diag > up > left (the a, b, c
+ *   order of serial.cpp:24-30's max).
+ */
+static inline int32_t imax(int32_t a, int32_t b) { return a > b ? a : b; }
+
+void nw_oracle_sw_fill(const int8_t *s1, int64_t n1, const int8_t *s2, int64_t n2,
+                       int32_t match, int32_t mismatch, int32_t gap, int32_t *t) {
+    const int64_t nCols = n1 + 1;
+    for (int64_t j = 0; j < nCols; ++j) t[j] = 0;
+    for (int64_t i = 1; i <= n2; ++i) {
+        int32_t *row = t + i * nCols;
+        const int32_t *up = row - nCols;
+        row[0] = 0;
+        for (int64_t j = 1; j < nCols; ++j) {
+            int32_t x = up[j - 1] + ref_sub(s1[j - 1], s2[i - 1], match, mismatch);
+            x = imax(x, up[j] + gap);
+            x = imax(x, row[j - 1] + gap);
+            row[j] = imax(x, 0);
+        }
+    }
+}
+
+/* Best cell in linear memory: returns the score, *end_i / *end_j = its first
+ * row-major position ((0, 0) when the table is all zero). */
+int32_t nw_oracle_sw_best(const int8_t *s1, int64_t n1, const int8_t *s2, int64_t n2,
+                          int32_t match, int32_t mismatch, int32_t gap, int64_t *end_i, int64_t *end_j) {
+    const int64_t nCols = n1 + 1;
+    int32_t *a = (int32_t *)calloc((size_t)nCols, sizeof(int32_t));
+    int32_t *b = (int32_t *)calloc((size_t)nCols, sizeof(int32_t));
+    int32_t best = 0;
+    *end_i = 0;
+    *end_j = 0;
+    if (!a || !b) { free(a); free(b); return -1; }
+    for (int64_t i = 1; i <= n2; ++i) {
+        b[0] = 0;
+        for (int64_t j = 1; j < nCols; ++j) {
+            int32_t x = a[j - 1] + ref_sub(s1[j - 1], s2[i - 1], match, mismatch);
+            x = imax(x, a[j] + gap);
+            x = imax(x, b[j - 1] + gap);
+            x = imax(x, 0);
+            b[j] = x;
+            if (x > best) { best = x; *end_i = i; *end_j = j; }
+        }
+        int32_t *tmp = a; a = b; b = tmp;
+    }
+    free(a);
+    free(b);
+    return best;
+}
+
+/* Traceback on a full SW table (pitch n1 + 1) from (end_i, end_j); ops in path
+ * order begin -> end (0 diag, 1 up, 2 left).  Returns the number of ops (-1 if
+ * cap is too small, -2 if t is not an SW table); *begin_i / *begin_j = where
+ * the walk reached t == 0. */
+int64_t nw_oracle_sw_traceback(const int8_t *s1, int64_t n1, const int8_t *s2, int64_t n2,
+                               int32_t match, int32_t mismatch, int32_t gap, const int32_t *t,
+                               int64_t end_i, int64_t end_j, uint8_t *ops, int64_t cap,
+                               int64_t *begin_i, int64_t *begin_j) {
+    const int64_t nCols = n1 + 1;
+    int64_t i = end_i, j = end_j, k = 0;
+    (void)n2;
+    while (i > 0 && j > 0 && t[i * nCols + j] > 0) {
+        const int32_t v = t[i * nCols + j];
+        uint8_t op;
+        if (v == t[(i - 1) * nCols + j - 1] + ref_sub(s1[j - 1], s2[i - 1], match, mismatch)) {
+            op = 0; --i; --j;
+        } else if (v == t[(i - 1) * nCols + j] + gap) {
+            op = 1; --i;
+        } else if (v == t[i * nCols + j - 1] + gap) {
+            op = 2; --j;
+        } else {
+            return -2;
+        }
+        if (k >= cap) return -1;
+        ops[k++] = op;
+    }
+    for (int64_t x = 0, y = k - 1; x < y; ++x, --y) { uint8_t tmp = ops[x]; ops[x] = ops[y]; ops[y] = tmp; }
+    *begin_i = i;
+    *begin_j = j;
+    return k;
+}

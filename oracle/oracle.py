@@ -61,6 +61,18 @@ def lib() -> ctypes.CDLL:
                                           ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                           ctypes.c_int, ctypes.c_int, _i32p, _i32p]
         L.nw_oracle_synth.argtypes = [ctypes.c_uint64, ctypes.c_int64, _i8p]
+        L.nw_oracle_sw_fill.argtypes = [_i8p, ctypes.c_int64, _i8p, ctypes.c_int64, ctypes.c_int32,
+                                        ctypes.c_int32, ctypes.c_int32, _i32p]
+        L.nw_oracle_sw_fill.restype = None
+        _i64p = ctypes.POINTER(ctypes.c_int64)
+        L.nw_oracle_sw_best.argtypes = [_i8p, ctypes.c_int64, _i8p, ctypes.c_int64, ctypes.c_int32,
+                                        ctypes.c_int32, ctypes.c_int32, _i64p, _i64p]
+        L.nw_oracle_sw_best.restype = ctypes.c_int32
+        L.nw_oracle_sw_traceback.argtypes = [_i8p, ctypes.c_int64, _i8p, ctypes.c_int64, ctypes.c_int32,
+                                             ctypes.c_int32, ctypes.c_int32, _i32p, ctypes.c_int64,
+                                             ctypes.c_int64, ctypes.POINTER(ctypes.c_uint8), ctypes.c_int64,
+                                             _i64p, _i64p]
+        L.nw_oracle_sw_traceback.restype = ctypes.c_int64
         _lib = L
     return _lib
 
@@ -83,6 +95,17 @@ def fill(s1, s2, scheme=(1, 0, -1)) -> np.ndarray:
     t = np.empty((b.size + 1, a.size + 1), dtype=np.int32)
     lib().nw_oracle_fill(_p(a, _i8p), a.size, _p(b, _i8p), b.size, *scheme, _p(t, _i32p), a.size + 1)
     return t
+
+
+def fill_emb(s1, s2, scheme=(1, 0, -1)) -> np.ndarray:
+    """The emb layout of src/idxarray/idxarray-emb-mt.cpp:4-65 (caller driver2.cpp:20-22):
+    (n2+1) x (n1+2); column 0 = the rows' progress counters at their final value
+    n1+2 (:36 row 0, :49 rows >= 1), columns 1.. = the serial table."""
+    t = fill(s1, s2, scheme)
+    out = np.empty((t.shape[0], t.shape[1] + 1), dtype=np.int32)
+    out[:, 0] = t.shape[1] + 1
+    out[:, 1:] = t
+    return out
 
 
 def fill_idxarray(s1, s2, scheme=(1, 0, -1), nthreads=8) -> np.ndarray:
@@ -124,6 +147,54 @@ def fill_band(s1, s2, P, r, halo, scheme=(1, 0, -1)) -> np.ndarray:
     return t
 
 
+# ------------------------------------------------------------------ Smith-Waterman
+# (config 5; no reference counterpart -- parity unpinned, nw_oracle.c documents the
+# conventions: 0 floor, first row-major best cell, traceback diag > up > left)
+def sw_fill(s1, s2, scheme=(1, -1, -1)) -> np.ndarray:
+    a, b = _seq(s1), _seq(s2)
+    t = np.empty((b.size + 1, a.size + 1), dtype=np.int32)
+    lib().nw_oracle_sw_fill(_p(a, _i8p), a.size, _p(b, _i8p), b.size, *scheme, _p(t, _i32p))
+    return t
+
+
+def sw_best(s1, s2, scheme=(1, -1, -1)):
+    """(score, end_i, end_j) in linear memory."""
+    a, b = _seq(s1), _seq(s2)
+    ei, ej = ctypes.c_int64(), ctypes.c_int64()
+    sc = lib().nw_oracle_sw_best(_p(a, _i8p), a.size, _p(b, _i8p), b.size, *scheme,
+                                 ctypes.byref(ei), ctypes.byref(ej))
+    return int(sc), int(ei.value), int(ej.value)
+
+
+def sw_traceback(s1, s2, t, end, scheme=(1, -1, -1)):
+    """(ops uint8 array begin -> end, begin_i, begin_j) from a full SW table."""
+    a, b = _seq(s1), _seq(s2)
+    t = np.ascontiguousarray(t, dtype=np.int32)
+    ops = np.empty(a.size + b.size + 1, dtype=np.uint8)
+    bi, bj = ctypes.c_int64(), ctypes.c_int64()
+    k = lib().nw_oracle_sw_traceback(_p(a, _i8p), a.size, _p(b, _i8p), b.size, *scheme, _p(t, _i32p),
+                                     end[0], end[1], ops.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
+                                     ops.size, ctypes.byref(bi), ctypes.byref(bj))
+    if k < 0:
+        raise ValueError(f"sw_traceback failed ({k})")
+    return ops[:k].copy(), int(bi.value), int(bj.value)
+
+
+def sw_path_score(s1, s2, ops, begin, scheme=(1, -1, -1)) -> int:
+    """Score of an alignment path (a size-independent property of a traceback):
+    the sum of the substitution / gap scores along ops from `begin`."""
+    a, b = _seq(s1), _seq(s2)
+    ops = np.asarray(ops, dtype=np.uint8)
+    m, mm, g = scheme
+    i, j = begin
+    di = np.where(ops == 2, 0, 1).cumsum()
+    dj = np.where(ops == 1, 0, 1).cumsum()
+    ii, jj = i + di, j + dj  # cell reached by each op
+    diag = ops == 0
+    eq = a[jj[diag] - 1] == b[ii[diag] - 1]
+    return int(np.where(eq, m, mm).sum() + g * int((~diag).sum()))
+
+
 def synth(seed: int, n: int) -> np.ndarray:
     out = np.empty(n, dtype=np.int8)
     lib().nw_oracle_synth(seed, n, _p(out, _i8p))
@@ -148,8 +219,10 @@ def ref_available(name: str = "libref_serial.so") -> bool:
     return os.path.exists(os.path.join(REF_DIR, name))
 
 
-def ref_fill(s1, s2, lib_name="libref_serial.so") -> np.ndarray:
-    """Run the reference's own needlemanWunsch (compiled from its sources) on s1 x s2."""
+def ref_fill(s1, s2, lib_name="libref_serial.so", extra_cols=0) -> np.ndarray:
+    """Run the reference's own needlemanWunsch (compiled from its sources) on s1 x s2
+    (extra_cols=1 for the emb-layout fills: n1+2 columns, driver2.cpp:20-22).  The
+    table starts zeroed (idxarray-emb-mt.cpp:13-15 reads t[1] before writing it)."""
     L = ctypes.CDLL(os.path.join(REF_DIR, lib_name))
     fn = getattr(L, "_Z15needlemanWunsch8dnaArrayS_Pi")
     fn.argtypes = [DnaArray, DnaArray, _i32p]
@@ -157,6 +230,6 @@ def ref_fill(s1, s2, lib_name="libref_serial.so") -> np.ndarray:
     a, b = _seq(s1), _seq(s2)
     a_buf = np.ascontiguousarray(a) if a.size else np.zeros(1, np.int8)
     b_buf = np.ascontiguousarray(b) if b.size else np.zeros(1, np.int8)
-    t = np.zeros((b.size + 1, a.size + 1), dtype=np.int32)
+    t = np.zeros((b.size + 1, a.size + 1 + extra_cols), dtype=np.int32)
     fn(DnaArray(a.size, _p(a_buf, _i8p)), DnaArray(b.size, _p(b_buf, _i8p)), _p(t, _i32p))
     return t

@@ -280,6 +280,37 @@ def test_config2_32k_vs_oracle(torch, ctx, strip):
     np.testing.assert_array_equal(grw, rw)
 
 
+# ------------------------------------------------------------------ emb layout
+@pytest.mark.parametrize("scheme", list(SCHEMES))
+@pytest.mark.parametrize("name", TINY + ["smid"])
+def test_emb_layout_vs_oracle(pair, scheme, name):
+    """nw_fill_emb: the driver2.cpp / idxarray-emb-mt table (n1+2 columns, progress
+    column 0 = n1+2, columns 1.. = serial), bit-exact."""
+    s1, s2 = pair(name)
+    import ctypes
+    t = np.full((s2.size + 1, s1.size + 2), -7, dtype=np.int32)
+    p = nwhip.params(SCHEMES[scheme])
+    L = nwhip.lib()
+    L.nw_fill_emb.argtypes = L.nw_fill.argtypes
+    i8 = ctypes.POINTER(ctypes.c_int8)
+    a, b = np.ascontiguousarray(s1), np.ascontiguousarray(s2)
+    st = L.nw_fill_emb(a.ctypes.data_as(i8), a.size, b.ctypes.data_as(i8), b.size, ctypes.byref(p),
+                       t.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), None)
+    assert st == nwhip.NW_OK
+    np.testing.assert_array_equal(t, oracle.fill_emb(s1, s2, SCHEMES[scheme]))
+
+
+@pytest.mark.parametrize("name", ["small", "t", "debug", "smid"])
+def test_dropin_driver_emb_cli(golden, name):
+    """build/nw_driver_emb: driver2.cpp's stdout is the wall milliseconds only (no
+    newline, no score), exit status 0."""
+    e = golden["pairs"][name]
+    out = subprocess.run([os.path.join(PKG, "build", "nw_driver_emb"), bdna_path(e["argv1"]),
+                          bdna_path(e["argv2"])], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.isdigit()
+
+
 # ------------------------------------------------------------------ drop-in CLI
 @pytest.mark.parametrize("drv,name,want", [("nw_driver", "small", 2), ("nw_driver", "t", 17),
                                            ("nw_driver", "debug", 27), ("nw_driver", "smid", 5839),

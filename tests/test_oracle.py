@@ -123,3 +123,15 @@ def test_band_partition_composes(n2, P):
         covered += nr - (r > 0)
     assert covered == n2 + 1
     np.testing.assert_array_equal(np.concatenate(rows), full)
+
+
+@pytest.mark.skipif(not oracle.ref_available("libref_idxarray_emb_mt.so"),
+                    reason="oracle/_ref not built (needs /root/reference)")
+@pytest.mark.parametrize("name", TINY + ["smid"])
+def test_emb_layout_matches_reference(pair, name):
+    """oracle.fill_emb (the restatement the GPU emb path is checked against) equals the
+    reference's own idxarray-emb-mt fill (src/idxarray/idxarray-emb-mt.cpp:4-65,
+    driver2.cpp:20-22 layout), progress column included."""
+    s1, s2 = pair(name)
+    want = oracle.ref_fill(s1, s2, "libref_idxarray_emb_mt.so", extra_cols=1)
+    np.testing.assert_array_equal(oracle.fill_emb(s1, s2), want)
