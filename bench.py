@@ -42,6 +42,11 @@ def parse():
     ap.add_argument("--band-rows", type=int, default=65536,
                     help="N>1: rows per GPU band (weak scaling; N=8 -> 512k x 512k, config 4)")
     ap.add_argument("--band-cols", type=int, default=524288, help="N>1: table columns n1")
+    ap.add_argument("--partition", choices=["rows", "cols"], default="rows",
+                    help="N>1: row bands (mpi-horz, config 4) or column bands (mpi-vert)")
+    ap.add_argument("--col-width", type=int, default=65536,
+                    help="N>1 column bands: columns per GPU (weak scaling; n1 = N x this)")
+    ap.add_argument("--col-rows", type=int, default=524288, help="N>1 column bands: table rows n2")
     ap.add_argument("--share-gpu", action="store_true",
                     help="N>1 rehearsal: every rank on device 0 (co-resident halves)")
     ap.add_argument("--workload", choices=["nw", "sw"], default="nw",

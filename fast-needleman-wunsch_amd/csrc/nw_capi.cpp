@@ -74,17 +74,28 @@ int grow(void **p, size_t *cap, size_t need, bool *fresh = nullptr) {
 
 struct Shape {
     int64_t nRows, nCols, nstrips, nblocks, waves, M, gstride;
+    int64_t waves_max;  // resident strip workgroups (before capping at nstrips)
     int32_t K, NC;
 };
 
 constexpr int kLdsPerCU = 160 * 1024;
 
 // Strip shape for nw_params.substrips = strip_waves = 0: the measured table of
-// tools/tune.py (csrc/nw_tuned.h, by table size), else (2, 2).
+// tools/tune.py (csrc/nw_tuned.h, by table size), else (2, 2).  The table is
+// measured on squares.  A table at least 4x wider than tall is bound by the
+// chain of strip-to-strip hand-offs (strips x hop latency) rather than by its
+// stores, and wants the shape with the shortest hop: measured with
+// tools/rect_time.py, 524288 x 8191 fills in 15.5 ms with (4,1) against 19.9
+// (2,2) and 29.7 (1,4); 524288 x 65535 in 33.0 ms with (2,2), 33.7 (4,1), 37.4 (1,4).
 void tuned_shape(int64_t n1, int64_t n2, int32_t *c, int32_t *nc) {
     const double cells = (double)(n1 + 1) * (double)(n2 + 1);
     *c = 2;
     *nc = 2;
+    if (n1 + 1 >= 4 * (n2 + 1) && n1 >= 65536) {
+        *c = n2 + 1 <= 32768 ? 4 : 2;
+        *nc = n2 + 1 <= 32768 ? 1 : 2;
+        return;
+    }
     for (const auto &e : nw::kTuned)
         if (cells >= e.min_cells && nw::shape_ok(e.c, e.nc)) {
             *c = e.c;
@@ -110,6 +121,7 @@ Shape make_shape(int64_t n1, int64_t n2, int32_t waves_req, int32_t sub_req, int
     // one strip workgroup per LDS ring set; as many as fit in a CU's LDS
     const int64_t per_cu = std::max(1, kLdsPerCU / nw::lds_bytes(s.K, s.NC));
     int64_t w = waves_req > 0 ? waves_req : per_cu * cus;
+    s.waves_max = std::max<int64_t>(1, w);
     s.waves = std::max<int64_t>(1, std::min<int64_t>(w, s.nstrips));
     // Strip p publishes into slot p % M.  When strip p is claimed, every strip
     // <= p - waves has finished, so M = waves + 1 slots never alias a live one.
@@ -233,14 +245,31 @@ void nw_ctx_destroy(nw_ctx *c) {
     delete c;
 }
 
+// Column band r of nbands (nw_colband_layout): strips [sf, sf + sc) of the whole
+// table's sweep (col0 = 1), local column 0 = global column start = sf * W.
+static int colband_layout(int64_t n1, int64_t n2, int32_t nb, int32_t r, const nw_params *p, int cus,
+                   int64_t *sf, int64_t *sc, int64_t *start, int64_t *ncols) {
+    if (!p || n1 < 1 || n2 < 0 || nb < 1 || r < 0 || r >= nb) return NW_ERR_ARG;
+    const Shape s = make_shape(n1, n2, 0, p->substrips, p->strip_waves, cus, 1);
+    if (!nw::shape_ok(s.K, s.NC) || nb > s.nstrips) return NW_ERR_ARG;
+    const int64_t W = (int64_t)nw::kWave * s.K * s.NC;
+    const int64_t base = s.nstrips / nb, extra = s.nstrips % nb;
+    *sf = r * base + std::min<int64_t>(r, extra);
+    *sc = base + (r < extra ? 1 : 0);
+    *start = *sf * W;
+    *ncols = std::min(*sc * W, n1 - *start) + 1;  // + the left column (band r-1's last)
+    return NW_OK;
+}
+
 static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *d_s2, int64_t n2,
-                       const nw_params *p, const nw_band *band, int32_t *d_t, int64_t pitch,
-                       void *stream) {
+                       const nw_params *p, const nw_band *band, const nw_colband *cb, int32_t *d_t,
+                       int64_t pitch, void *stream) {
     if (!c || !d_t || n1 < 0 || n2 < 0 || n1 >= INT32_MAX || n2 >= INT32_MAX) return NW_ERR_ARG;
     if ((n1 > 0 && !d_s1) || (n2 > 0 && !d_s2)) return NW_ERR_ARG;
     if (!valid_params(p)) return NW_ERR_ARG;
     const bool sw = p->mode == NW_MODE_SW;
-    if (sw && band) return NW_ERR_UNSUPPORTED;  // (local alignment: single table, config 5)
+    if (sw && (band || cb)) return NW_ERR_UNSUPPORTED;  // (local alignment: single table, config 5)
+    if (band && cb) return NW_ERR_ARG;
     // The kernel holds w = t - GAP*(i+j) in int32 next to a "minus infinity" of
     // -2^29: |w| <= (max|score| + |GAP|) * (i + j) must stay below 2^28, with i the
     // GLOBAL row (a band's halo row carries the values of row band->row0).
@@ -253,27 +282,47 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
         const long long i_max = (long long)n2 + (band ? (long long)band->row0 : 0);
         if ((m + std::llabs(p->gap)) * (long long)(n1 + i_max + 2) >= (1LL << 28)) return NW_ERR_ARG;
     }
-    // any 64-multiple pitch that holds nCols = n1 + 1 (nw_table_pitch adds the
-    // slack that lets the strips start at column 1)
-    if (pitch < n1 + 1 || pitch % nw::kWave != 0) return NW_ERR_ARG;
-    // Strip origin: column 1 when the base is laid out so that column 1 starts a
-    // 256-byte line (nw_table_offset), which takes the boundary column 0 out of
-    // the sweep; column 0 for a 256-byte aligned base.  Anything else is refused.
     int64_t col0;
-    if ((((uintptr_t)d_t + 4u) & 255u) == 0 && n1 >= 1 && pitch >= n1 + 4)
+    int64_t strip_first = 0, strip_count = 0, start = 0;
+    if (cb) {
+        // a column band's local table: the nw_table_offset layout over its n_cols
+        // columns (local column 1 starts a 256-byte line, as in every band)
+        if (cb->tag == 0 || (((uintptr_t)cb->feed_in | (uintptr_t)cb->feed_out) & 7u) != 0) return NW_ERR_ARG;
+        int64_t ncols = 0;
+        int st0 = colband_layout(n1, n2, cb->nbands, cb->r, p, c->cus, &strip_first, &strip_count, &start, &ncols);
+        if (st0 != NW_OK) return st0;
+        if ((cb->r > 0) != (cb->feed_in != nullptr) || (cb->r + 1 < cb->nbands) != (cb->feed_out != nullptr))
+            return NW_ERR_ARG;
+        if (cb->feed_out && (p->flags & 1)) return NW_ERR_ARG;  // needs the real right column
+        if ((((uintptr_t)d_t + 4u) & 255u) != 0 || pitch % nw::kWave != 0 || pitch < ncols + 3) return NW_ERR_ARG;
         col0 = 1;
-    else if (((uintptr_t)d_t & 255u) == 0)
-        col0 = 0;
-    else
-        return NW_ERR_ARG;
+    } else {
+        // any 64-multiple pitch that holds nCols = n1 + 1 (nw_table_pitch adds the
+        // slack that lets the strips start at column 1)
+        if (pitch < n1 + 1 || pitch % nw::kWave != 0) return NW_ERR_ARG;
+        // Strip origin: column 1 when the base is laid out so that column 1 starts a
+        // 256-byte line (nw_table_offset), which takes the boundary column 0 out of
+        // the sweep; column 0 for a 256-byte aligned base.  Anything else is refused.
+        if ((((uintptr_t)d_t + 4u) & 255u) == 0 && n1 >= 1 && pitch >= n1 + 4)
+            col0 = 1;
+        else if (((uintptr_t)d_t & 255u) == 0)
+            col0 = 0;
+        else
+            return NW_ERR_ARG;
+    }
     if (band) {
         if (band->tag == 0 || (((uintptr_t)band->halo_in | (uintptr_t)band->halo_out) & 7u) != 0)
             return NW_ERR_ARG;
         if (band->halo_out && (p->flags & 1)) return NW_ERR_ARG;  // needs the real last row
     }
     NW_HIP_TRY(hipSetDevice(c->device));
-    const Shape s = make_shape(n1, n2, p->waves, p->substrips, p->strip_waves, c->cus, col0);
+    Shape s = make_shape(n1, n2, p->waves, p->substrips, p->strip_waves, c->cus, col0);
     if (!nw::shape_ok(s.K, s.NC)) return NW_ERR_ARG;
+    if (cb) {  // this launch sweeps its band's strips only
+        s.nstrips = strip_count;
+        s.waves = std::max<int64_t>(1, std::min<int64_t>(s.waves_max, s.nstrips));
+        s.M = std::min<int64_t>(s.nstrips, s.waves + 1);
+    }
     if (sw && !nw::sw_shape_ok(s.K, s.NC)) return NW_ERR_UNSUPPORTED;
     if (s.nstrips > INT32_MAX / 2 || s.nblocks > INT32_MAX / 2) return NW_ERR_ARG;
 
@@ -320,8 +369,13 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
 
     nw::FillArgs a;
     std::memset(&a, 0, sizeof a);
-    a.table = d_t;
+    a.table = d_t - start;  // table + c = global column c (start = 0 but for column bands)
     a.pitch = pitch;
+    a.col_end = start + pitch;
+    a.strip0 = (int32_t)strip_first;
+    a.feed_in = cb ? cb->feed_in : nullptr;
+    a.feed_out = cb ? cb->feed_out : nullptr;
+    a.feed_tag = cb ? cb->tag : 0u;
     a.rowpack = c->rowpack;
     a.s1 = n1 > 0 ? (const uint8_t *)d_s1 : (const uint8_t *)c->ctrl;
     a.n1 = n1;
@@ -352,6 +406,10 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
     a.sw = sw ? 1 : 0;
     a.smax = sw ? c->smax : nullptr;
     if (nw::launch_fill(a, s.K, s.NC, (int)s.waves, stream) != hipSuccess) return NW_ERR_HIP;
+    // a column band's local column 0 (band r-1's last column) from its feed
+    if (cb && cb->feed_in &&
+        nw::launch_colband_edge(cb->feed_in, d_t, pitch, n2, p->gap, start, stream) != hipSuccess)
+        return NW_ERR_HIP;
     c->tagbase += (uint32_t)s.nstrips + 1u;
     c->last_waves = (int)s.waves;
     c->last_strips = (int)s.nstrips;
@@ -373,14 +431,14 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
 int nw_fill_device_async(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *d_s2,
                          int64_t n2, const nw_params *p, int32_t *d_t, int64_t pitch,
                          void *stream) {
-    return launch_fill(c, d_s1, n1, d_s2, n2, p, nullptr, d_t, pitch, stream);
+    return launch_fill(c, d_s1, n1, d_s2, n2, p, nullptr, nullptr, d_t, pitch, stream);
 }
 
 int nw_fill_band_async(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *d_s2_band,
                        int64_t n2_band, const nw_params *p, const nw_band *band, int32_t *d_t,
                        int64_t pitch, void *stream) {
     if (!band) return NW_ERR_ARG;
-    return launch_fill(c, d_s1, n1, d_s2_band, n2_band, p, band, d_t, pitch, stream);
+    return launch_fill(c, d_s1, n1, d_s2_band, n2_band, p, band, nullptr, d_t, pitch, stream);
 }
 
 void nw_band_layout(int64_t n2, int32_t nbands, int32_t r, int64_t *n_rows, int64_t *start) {
@@ -394,6 +452,44 @@ void nw_band_layout(int64_t n2, int32_t nbands, int32_t r, int64_t *n_rows, int6
     }
     if (n_rows) *n_rows = rows;
     if (start) *start = st;
+}
+
+int nw_colband_layout(int64_t n1, int64_t n2, int32_t nbands, int32_t r, const nw_params *p,
+                      int64_t *strip_first, int64_t *strip_count, int64_t *start, int64_t *n_cols) {
+    int64_t sf = 0, sc = 0, st = 0, nc = 0;
+    const int rc = colband_layout(n1, n2, nbands, r, p, 256, &sf, &sc, &st, &nc);
+    if (strip_first) *strip_first = sf;
+    if (strip_count) *strip_count = sc;
+    if (start) *start = st;
+    if (n_cols) *n_cols = nc;
+    return rc;
+}
+
+int nw_fill_colband_async(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *d_s2, int64_t n2,
+                          const nw_params *p, const nw_colband *band, int32_t *d_t, int64_t pitch,
+                          void *stream) {
+    if (!band) return NW_ERR_ARG;
+    return launch_fill(c, d_s1, n1, d_s2, n2, p, nullptr, band, d_t, pitch, stream);
+}
+
+int64_t nw_feed_bytes(int64_t n2) {
+    return n2 < 0 ? 0 : round_up(n2 + 1, nw::kWave) * (int64_t)sizeof(uint64_t);
+}
+
+int nw_feed_alloc(int device, int64_t n2, uint64_t **d_feed) {
+    if (!d_feed || n2 < 0) return NW_ERR_ARG;
+    *d_feed = nullptr;
+    if (device >= 0) NW_HIP_TRY(hipSetDevice(device));
+    void *q = nullptr;
+    const size_t bytes = (size_t)nw_feed_bytes(n2);
+    hipError_t e = hipMalloc(&q, bytes);
+    if (e != hipSuccess) return e == hipErrorOutOfMemory ? NW_ERR_OOM : NW_ERR_HIP;
+    if (hipMemset(q, 0, bytes) != hipSuccess) {
+        (void)hipFree(q);
+        return NW_ERR_HIP;
+    }
+    *d_feed = (uint64_t *)q;
+    return NW_OK;
 }
 
 int64_t nw_halo_bytes(int64_t n1) { return n1 < 0 ? 0 : (n1 + 1) * (int64_t)sizeof(uint64_t); }

@@ -172,11 +172,13 @@ static_assert(Lay<4, 1>::kBytes <= 160 * 1024, "ring must fit a CU's LDS");
 static_assert(Lay<2, 2>::kBytes <= 160 * 1024, "ring must fit a CU's LDS");
 static_assert(Lay<1, 4>::kBytes <= 160 * 1024, "ring must fit a CU's LDS");
 
+// Granules are system-scope: the same loads and stores serve a column band's
+// feed, which lives in the neighbouring GPU's HBM (written over xGMI).
 __device__ __forceinline__ uint64_t gran_load(const uint64_t *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ void gran_store(uint64_t *p, uint64_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ uint32_t ctrl_load(const uint32_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -662,7 +664,10 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
     F.src = j > 0 ? FEED_LDS : p > 0 ? FEED_GRAN : FEED_BOUNDARY;
     F.ring = (int32_t *)(lds + L::kFeed) + j * kFeedRows;
     F.pub = (const int32_t *)(lds + L::kCtl) + (j > 0 ? j - 1 : 0) * L::kCtlWords + 1;
-    F.tag = A.tagbase + (uint32_t)p;
+    // a column band's first strip is fed by the left band (feed_in, feed_tag)
+    const bool fed = p == A.strip0 && A.feed_in != nullptr;
+    const bool feeds = p == A.strip0 + A.nstrips - 1 && A.feed_out != nullptr;
+    F.tag = fed ? A.feed_tag : A.tagbase + (uint32_t)p;
     F.gap = gap;
     F.nslow = 0;
     F.wticks = 0;
@@ -678,9 +683,9 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
     O.gap = gap;
     const int32_t *next_done = ctr + L::kCtlWords + 2;  // iterations done by wave j+1
 
-    const uint64_t *gin = A.gran + (int64_t)((p + A.M - 1) % A.M) * A.gstride + lane;
-    uint64_t *gout = A.gran + (int64_t)(p % A.M) * A.gstride;
-    const uint64_t tagw = (uint64_t)(A.tagbase + (uint32_t)p + 1u) << 32;
+    const uint64_t *gin = (fed ? A.feed_in : A.gran + (int64_t)((p + A.M - 1) % A.M) * A.gstride) + lane;
+    uint64_t *gout = feeds ? A.feed_out : A.gran + (int64_t)(p % A.M) * A.gstride;
+    const uint64_t tagw = (uint64_t)(feeds ? A.feed_tag : A.tagbase + (uint32_t)p + 1u) << 32;
     const int nblocks = A.nblocks;
     const int lastb = nblocks - 1;
     uint64_t *gscr = (uint64_t *)(A.scratch + (int64_t)blockIdx.x * kScratchWords) + lane;
@@ -793,7 +798,7 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
     ctr_store(ctr + 1, kDone);
     ctr_store(ctr + 2, kDone);
     if (A.trace != nullptr && lane == 0) {
-        uint64_t *tr = A.trace + (int64_t)p * kTraceWords;
+        uint64_t *tr = A.trace + (int64_t)(p - A.strip0) * kTraceWords;
         if (j == 0) {
             tr[0] = tstart;
             tr[2] = F.nslow;
@@ -855,7 +860,7 @@ __device__ __forceinline__ void store_strip(const FillArgs &A, char *__restrict_
     // the last strip may overhang the pitch: store only 16-byte pieces that lie
     // wholly inside the row (with col0 = 1 a piece straddling the pitch would
     // reach the next row's column 0; nw_table_pitch leaves room for column n1)
-    const bool col_ok = c0 + 4 * cq + 4 <= A.pitch;
+    const bool col_ok = c0 + 4 * cq + 4 <= A.col_end;
     const int64_t rowb = timing ? 0 : A.pitch * 4;
     char *scr = (char *)(A.scratch + (int64_t)blockIdx.x * kScratchWords);
     const int32_t f0 = q * BATCH;
@@ -1025,7 +1030,7 @@ __device__ __forceinline__ void store_strip_grp(const FillArgs &A, char *__restr
     // the last strip may overhang the pitch: store only 16-byte pieces wholly inside the row
     bool col_ok[2];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) col_ok[h] = c0 + 32 * h + 4 * cq + 4 <= A.pitch;
+    for (int h = 0; h < 2; ++h) col_ok[h] = c0 + 32 * h + 4 * cq + 4 <= A.col_end;
     // SW: running maximum of this lane's cells (columns <= n1) for A.smax[p]
     uint32_t cval = 0;
 #pragma unroll
@@ -1160,7 +1165,7 @@ __device__ __forceinline__ void store_strip_grp(const FillArgs &A, char *__restr
     ctr_store(mine, kDone);
     if (A.sw) strip_max(A, p, vmax);
     if (trace && lane == 0) {
-        uint64_t *trw = A.trace + (int64_t)p * kTraceWords;
+        uint64_t *trw = A.trace + (int64_t)(p - A.strip0) * kTraceWords;
         trw[16] = tw;
         trw[17] = 0;
         trw[18] = ts;
@@ -1207,8 +1212,9 @@ __global__ __launch_bounds__((64 * Lay<C, NC>::kWaves)) void nw_fill_strips(Fill
             ctl[L::kStripWord] = (int32_t)atomicAdd(A.ctrl, 1u);
         }
         __syncthreads();
-        const int p = __builtin_amdgcn_readfirstlane(ctl[L::kStripWord]);
-        if (p >= A.nstrips) break;
+        const int t = __builtin_amdgcn_readfirstlane(ctl[L::kStripWord]);
+        if (t >= A.nstrips) break;
+        const int p = A.strip0 + t;  // global strip index
         if (wave < NC) {
             // table form when the launch allows it (scores fit int8) and s1 has
             // at most kMaxPerm distinct characters (nw_charmap), else compares
@@ -1299,6 +1305,26 @@ __global__ void nw_rowpack(const uint8_t *__restrict__ s2, int64_t n2, int64_t r
         v[k >> 2] |= b << (8 * (k & 3));
     }
     q[idx] = v;
+}
+
+// Column band: local column 0 of the band's table = the left band's last column,
+// from the feed granules (w form) this launch consumed -- all of them, so their
+// values are final; system-scope loads as in the kernel (peer-written memory).
+__global__ __launch_bounds__(256) void nw_colband_edge(const uint64_t *__restrict__ feed,
+                                                       int32_t *__restrict__ table, int64_t pitch,
+                                                       int64_t n2, int32_t gap, int64_t start) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i > n2) return;
+    const uint64_t g = __hip_atomic_load(feed + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    table[i * pitch] = (int32_t)((int64_t)(int32_t)(uint32_t)g + (int64_t)gap * (i + start));
+}
+
+int launch_colband_edge(const uint64_t *feed, int32_t *table, int64_t pitch, int64_t n2, int32_t gap,
+                        int64_t start, void *stream) {
+    const int64_t rows = n2 + 1;
+    hipLaunchKernelGGL(nw_colband_edge, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       feed, table, pitch, n2, gap, start);
+    return (int)hipGetLastError();
 }
 
 // entries of 16 bytes: iteration j <= nblocks + 3 (prefetch of the last one)

@@ -54,8 +54,24 @@ struct FillArgs {
     // store waves fold each strip's best cell into smax[p] (zeroed before launch)
     int32_t sw;
     int32_t *smax;
+    // Column bands (mpi-vert contract): this launch sweeps global strips
+    // strip0 .. strip0 + nstrips - 1 of the table; `table` is biased so that
+    // table + c addresses global column c, and stores stay below column col_end.
+    // feed_in: the left neighbour band's last strip's right column (granules
+    // {tag:32 | w:32}, gstride of them, NULL = strip0's feed is the internal one
+    // or the boundary); feed_out: where this launch's last strip publishes its
+    // right column (peer memory; NULL = internal slot).  Both carry feed_tag.
+    int32_t strip0;
+    int64_t col_end;
+    const uint64_t *feed_in;
+    uint64_t *feed_out;
+    uint32_t feed_tag;
 };
 bool sw_shape_ok(int substrips, int strip_waves);
+// column band r > 0: local column 0 (global column `start`) from the feed
+// granules, t = w + gap * (i + start), rows 0..n2; asynchronous on `stream`
+int launch_colband_edge(const uint64_t *feed, int32_t *table, int64_t pitch, int64_t n2, int32_t gap,
+                        int64_t start, void *stream);
 // best cell of an SW table: reduce smax[nstrips] and find the first row-major cell
 // holding the maximum (out8[0] = score, out8[1..2] = row, out8[3..4] = column as
 // 64-bit halves); device buffers, asynchronous on `stream`

@@ -102,6 +102,83 @@ class LocalBands:
             c.close()
 
 
+# Per-row pace (ns) of a strip in a store-saturated sweep, per strip shape (C, NC):
+# tools/rect_time.py on 65536 x 524288 (one pass of 256 strips): T = pace *
+# (n2 + 255 * 64 * NC) gives (4,1) 35.2 ms -> 65, (2,2) 33.1 -> 59.4, (1,4) 30.0 -> 50.9.
+# The three shapes share the strip width W = 256 columns.
+COLBAND_PACE_NS = {(4, 1): 65.0, (2, 2): 59.4, (1, 4): 50.9}
+
+
+def colband_model_ms(n1: int, n2: int, shape) -> float:
+    """Critical path of a column-band sweep (multi-GPU model): strip p
+    starts one hop (64 * NC rows of the anti-diagonal skew) after strip p-1, so the
+    last of S strips starts (S-1) hops in and then runs all n2 rows."""
+    c, nc = shape
+    strips = -(-n1 // (64 * c * nc))
+    return COLBAND_PACE_NS[shape] * ((strips - 1) * 64 * nc + n2 + 1) * 1e-6
+
+
+def colband_shape(n1: int, n2: int, substrips: int = 0, strip_waves: int = 0):
+    """The strip shape of a column-band fill: the caller's, else the one of the
+    W = 256 shapes whose modelled critical path is shortest (a chain of many strips
+    wants the short hop of (4,1), a short chain the fast pace of (1,4))."""
+    if substrips or strip_waves:
+        return nwhip.strip_shape(substrips, strip_waves, n1, n2)
+    return min(COLBAND_PACE_NS, key=lambda sh: colband_model_ms(n1, n2, sh))
+
+
+class LocalColBands:
+    """P column bands of one (n2+1) x (n1+1) table on one device, filled concurrently
+    (src/mpi/mpi-vert.cpp's partition, the bands being whole strips of the table's
+    sweep): band r's table holds global columns [start_r, start_r + n_cols_r), its
+    local column 0 is band r-1's last column, fed to band r's first strip through a
+    feed buffer as band r-1's last strip produces it.  Each band gets 1/P of the
+    resident workers so that all bands are co-resident."""
+
+    def __init__(self, n1: int, n2: int, nbands: int, device: int = 0, substrips: int = 0,
+                 strip_waves: int = 0):
+        import torch
+        self.n1, self.n2, self.P, self.device = n1, n2, nbands, device
+        # one shape for every band (auto: colband_shape)
+        self.substrips, self.strip_waves = colband_shape(n1, n2, substrips, strip_waves)
+        self.layout = [nwhip.colband_layout(n1, n2, nbands, r, self.substrips, self.strip_waves)
+                       for r in range(nbands)]
+        self.tables = [nwhip.Context.alloc_table(nc - 1, n2) for _, _, _, nc in self.layout]
+        self.feeds = [None] + [nwhip.Feed(n2, device) for _ in range(nbands - 1)]
+        self.ctxs = [nwhip.Context(device) for _ in range(nbands)]
+        self.streams = [torch.cuda.Stream(device) for _ in range(nbands)]
+        self.waves = max(1, resident_waves(device, self.substrips, self.strip_waves) // nbands)
+        self.tag = 0
+
+    def fill(self, d_s1, d_s2, scheme=(1, 0, -1), flags: int = 0, timeout_ms: int = 0) -> int:
+        """Fill every band; returns the final score t[n2][n1] (last band's last cell)."""
+        import torch
+        assert int(d_s1.numel()) == self.n1 and int(d_s2.numel()) == self.n2
+        self.tag += 1
+        cur = torch.cuda.current_stream(self.device)
+        for r, st in enumerate(self.streams):
+            st.wait_stream(cur)
+            self.ctxs[r].fill_colband(
+                d_s1, d_s2, self.tables[r], self.P, r,
+                feed_in=self.feeds[r].ptr if r > 0 else None,
+                feed_out=self.feeds[r + 1].ptr if r + 1 < self.P else None,
+                tag=self.tag, scheme=scheme, waves=self.waves, stream=st, flags=flags,
+                substrips=self.substrips, strip_waves=self.strip_waves, timeout_ms=timeout_ms)
+        for r, st in enumerate(self.streams):
+            s = self.ctxs[r].status(st)
+            if s != nwhip.NW_OK:
+                raise nwhip.NwError(s, f"column band {r}")
+            cur.wait_stream(st)
+        return int(self.tables[-1][self.n2, self.layout[-1][3] - 1].item())
+
+    def close(self):
+        for f in self.feeds:
+            if f is not None:
+                f.free()
+        for c in self.ctxs:
+            c.close()
+
+
 # ----------------------------------------------------------------------- multi-process
 def _env_int(name: str, default: int) -> int:
     v = os.environ.get(name)
@@ -138,24 +215,36 @@ def run_bands(args) -> dict | None:
     if not dist.is_initialized():
         dist.init_process_group("gloo", rank=rank, world_size=world)
     scheme = tuple(int(x) for x in args.scheme.split(","))
-    n1 = args.band_cols
-    n2 = world * args.band_rows
-    rows, start = nwhip.band_layout(n2, world, rank)
-
-    # synthetic inputs, identical on every rank (seeds 1 / 2); this rank's side chars only
-    s1 = torch.from_numpy(nwhip.synth(1, n1)).cuda()
-    s2_band = torch.from_numpy(nwhip.synth(2, n2)[start:start + rows - 1].copy()).cuda()
-    table = nwhip.Context.alloc_table(n1, rows - 1)
+    cols = getattr(args, "partition", "rows") == "cols"
     ctx = nwhip.Context(dev)
-    halo_in = nwhip.Halo(n1, dev) if rank > 0 else None
+    stream = torch.cuda.current_stream()
+    if cols:
+        # column bands (mpi-vert): rank r owns ~col_width columns of every row
+        n1, n2 = world * args.col_width, args.col_rows
+        sub, nc = colband_shape(n1, n2, args.substrips, args.strip_waves)
+        sf, scount, start, ncols = nwhip.colband_layout(n1, n2, world, rank, sub, nc)
+        s1 = torch.from_numpy(nwhip.synth(1, n1)).cuda()
+        s2 = torch.from_numpy(nwhip.synth(2, n2)).cuda()
+        table = nwhip.Context.alloc_table(ncols - 1, n2)
+        link_in = nwhip.Feed(n2, dev) if rank > 0 else None
+        rows = n2 + 1
+    else:
+        n1 = args.band_cols
+        n2 = world * args.band_rows
+        rows, start = nwhip.band_layout(n2, world, rank)
+        # synthetic inputs, identical on every rank (seeds 1 / 2); this rank's side chars only
+        s1 = torch.from_numpy(nwhip.synth(1, n1)).cuda()
+        s2 = torch.from_numpy(nwhip.synth(2, n2)[start:start + rows - 1].copy()).cuda()
+        table = nwhip.Context.alloc_table(n1, rows - 1)
+        link_in = nwhip.Halo(n1, dev) if rank > 0 else None
+        sub, nc = nwhip.strip_shape(args.substrips, args.strip_waves, n1, rows - 1)
+    # each rank exports its incoming buffer; rank r-1 maps it and stores into it
     handles = [None] * world
-    dist.all_gather_object(handles, nwhip.ipc_get_handle(halo_in.ptr) if halo_in else None)
-    halo_out = nwhip.ipc_open_handle(handles[rank + 1]) if rank + 1 < world else None
-    sub, nc = nwhip.strip_shape(args.substrips, args.strip_waves, n1, rows - 1)
+    dist.all_gather_object(handles, nwhip.ipc_get_handle(link_in.ptr) if link_in else None)
+    link_out = nwhip.ipc_open_handle(handles[rank + 1]) if rank + 1 < world else None
     waves = args.waves
     if args.share_gpu and waves == 0:
         waves = max(1, resident_waves(dev, sub, nc) // world)
-    stream = torch.cuda.current_stream()
     tag = 0
 
     def step(ev=None):
@@ -163,14 +252,19 @@ def run_bands(args) -> dict | None:
         tag += 1
         if ev is not None:
             ev[0].record(stream)
-        ctx.fill_band(s1, s2_band, table, halo_in=halo_in.ptr if halo_in else None,
-                      halo_out=halo_out, tag=tag, scheme=scheme, waves=waves, stream=stream,
-                      substrips=sub, strip_waves=nc, row0=start)
+        if cols:
+            ctx.fill_colband(s1, s2, table, world, rank, feed_in=link_in.ptr if link_in else None,
+                             feed_out=link_out, tag=tag, scheme=scheme, waves=waves, stream=stream,
+                             substrips=sub, strip_waves=nc)
+        else:
+            ctx.fill_band(s1, s2, table, halo_in=link_in.ptr if link_in else None,
+                          halo_out=link_out, tag=tag, scheme=scheme, waves=waves, stream=stream,
+                          substrips=sub, strip_waves=nc, row0=start)
         if ev is not None:
             ev[1].record(stream)
         torch.cuda.synchronize()
-        # no rank starts launch k+1 (which rewrites its neighbour's halo) before every
-        # rank has finished launch k
+        # no rank starts launch k+1 (which rewrites its neighbour's halo / feed)
+        # before every rank has finished launch k
         dist.barrier()
 
     for _ in range(args.warmup):
@@ -190,14 +284,15 @@ def run_bands(args) -> dict | None:
     kms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     st_all = [None] * world
     dist.all_gather_object(st_all, (status, kms, rows, start))
-    score = int(table[rows - 1, n1].item()) if rank == world - 1 else None
+    last_col = (ncols - 1) if cols else n1
+    score = int(table[rows - 1, last_col].item()) if rank == world - 1 else None
     scores = [None] * world
     dist.all_gather_object(scores, score)
-    if halo_out is not None:
-        nwhip.ipc_close_handle(halo_out)
+    if link_out is not None:
+        nwhip.ipc_close_handle(link_out)
     dist.barrier()
-    if halo_in is not None:
-        halo_in.free()
+    if link_in is not None:
+        link_in.free()
     ctx.close()
     if any(s[0] != 0 for s in st_all):
         raise RuntimeError(f"band status per rank: {[s[0] for s in st_all]}")
@@ -225,13 +320,20 @@ def run_bands(args) -> dict | None:
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic (i.i.d. uniform {1,2,3,4}, seeds 1/2)",
-        "config": {"workload": f"nw_fill_rowbands_{n2}x{n1}", "n1": n1, "n2": n2,
-                   "scheme": list(scheme), "band_rows": args.band_rows, "bands": world,
-                   "table_bytes": int(table_bytes), "parallelism": f"row bands x{world}",
-                   "halo": f"in-kernel xGMI peer stores, one strip ({64 * sub * nc} columns) at a time",
-                   "strip_shape": [sub, nc],
-                   "control_plane": "torch.distributed gloo",
-                   "shared_gpu": bool(args.share_gpu)},
+        "config": ({"workload": f"nw_fill_colbands_{n2}x{n1}", "n1": n1, "n2": n2,
+                    "scheme": list(scheme), "col_width": args.col_width, "bands": world,
+                    "table_bytes": int(table_bytes), "parallelism": f"column bands x{world}",
+                    "halo": "in-kernel xGMI peer stores of the band's right column, 64 rows at a time",
+                    "strip_shape": [sub, nc],
+                    "control_plane": "torch.distributed gloo",
+                    "shared_gpu": bool(args.share_gpu)} if cols else
+                   {"workload": f"nw_fill_rowbands_{n2}x{n1}", "n1": n1, "n2": n2,
+                    "scheme": list(scheme), "band_rows": args.band_rows, "bands": world,
+                    "table_bytes": int(table_bytes), "parallelism": f"row bands x{world}",
+                    "halo": f"in-kernel xGMI peer stores, one strip ({64 * sub * nc} columns) at a time",
+                    "strip_shape": [sub, nc],
+                    "control_plane": "torch.distributed gloo",
+                    "shared_gpu": bool(args.share_gpu)}),
         "score": score,
         "score_golden": want,
         "score_ok": (want == score) if want is not None else None,

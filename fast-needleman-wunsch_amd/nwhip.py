@@ -31,7 +31,8 @@ EXPORTS = ["nw_params_default", "nw_strerror", "nw_version", "nw_fill", "nw_tabl
            "nw_synth_bdna", "nw_band_layout", "nw_halo_bytes", "nw_fill_band_async",
            "nw_ipc_get_handle", "nw_ipc_open_handle", "nw_ipc_close_handle", "nw_halo_alloc",
            "nw_halo_free", "nw_fill_emb", "nw_sw_align", "nw_sw_traceback", "nw_tuned_shape", "nw_debug_ctrl", "nw_debug_set_trace",
-           "nw_debug_trace_words"]
+           "nw_debug_trace_words", "nw_colband_layout", "nw_feed_bytes", "nw_feed_alloc",
+           "nw_fill_colband_async"]
 IPC_HANDLE_BYTES = 64
 
 
@@ -61,6 +62,12 @@ class NwBand(ctypes.Structure):
     """nw_band (include/nw_hip.h): halo granule buffers of one row band."""
     _fields_ = [("halo_in", ctypes.c_void_p), ("halo_out", ctypes.c_void_p),
                 ("tag", ctypes.c_uint32), ("row0", ctypes.c_uint32)]
+
+
+class NwColBand(ctypes.Structure):
+    """nw_colband (include/nw_hip.h): feed granule buffers of one column band."""
+    _fields_ = [("feed_in", ctypes.c_void_p), ("feed_out", ctypes.c_void_p), ("tag", ctypes.c_uint32),
+                ("nbands", ctypes.c_int32), ("r", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 class NwError(RuntimeError):
@@ -146,6 +153,15 @@ def lib() -> ctypes.CDLL:
     L.nw_tuned_shape.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(ctypes.c_int32),
                                  ctypes.POINTER(ctypes.c_int32)]
     L.nw_tuned_shape.restype = None
+    _i64p = ctypes.POINTER(ctypes.c_int64)
+    L.nw_colband_layout.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                    ctypes.POINTER(NwParams), _i64p, _i64p, _i64p, _i64p]
+    L.nw_feed_bytes.argtypes = [ctypes.c_int64]
+    L.nw_feed_bytes.restype = ctypes.c_int64
+    L.nw_feed_alloc.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p)]
+    L.nw_fill_colband_async.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                        ctypes.c_int64, ctypes.POINTER(NwParams), ctypes.POINTER(NwColBand),
+                                        ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
     L.nw_debug_ctrl.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32)]
     L.nw_debug_set_trace.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     L.nw_debug_trace_words.argtypes = []
@@ -302,6 +318,23 @@ def band_layout(n2: int, nbands: int, r: int):
     return int(rows.value), int(start.value)
 
 
+def colband_layout(n1: int, n2: int, nbands: int, r: int, substrips: int = 0, strip_waves: int = 0):
+    """(strip_first, strip_count, start, n_cols) of column band r: its strips of the
+    whole table's sweep and the global columns [start, start + n_cols) of its local
+    table, local column 0 = band r-1's last column (src/mpi/mpi-vert.cpp:17,
+    mpi-vert-driver.cpp:35-36, at strip granularity)."""
+    p = params(substrips=substrips, strip_waves=strip_waves)
+    out = [ctypes.c_int64() for _ in range(4)]
+    st = lib().nw_colband_layout(n1, n2, nbands, r, ctypes.byref(p), *[ctypes.byref(x) for x in out])
+    if st != NW_OK:
+        raise NwError(st, "nw_colband_layout")
+    return tuple(int(x.value) for x in out)
+
+
+def feed_bytes(n2: int) -> int:
+    return int(lib().nw_feed_bytes(n2))
+
+
 def halo_bytes(n1: int) -> int:
     return int(lib().nw_halo_bytes(n1))
 
@@ -326,6 +359,17 @@ class Halo:
             self.free()
         except Exception:
             pass
+
+
+class Feed(Halo):
+    """A zeroed column-band feed granule buffer (n2+1 rows, padded to 64, x {tag, value})."""
+
+    def __init__(self, n2: int, device: int = -1):
+        ptr = ctypes.c_void_p()
+        st = lib().nw_feed_alloc(device, n2, ctypes.byref(ptr))
+        if st != NW_OK:
+            raise NwError(st, "nw_feed_alloc")
+        self.ptr, self.n2 = int(ptr.value), n2
 
 
 def ipc_get_handle(ptr: int) -> bytes:
@@ -454,6 +498,27 @@ class Context:
                                       ctypes.c_void_p(stream.cuda_stream))
         if st != NW_OK:
             raise NwError(st, "nw_fill_band_async")
+
+    def fill_colband(self, d_s1, d_s2, table, nbands: int, r: int, feed_in=None, feed_out=None,
+                     tag: int = 1, scheme=(1, 0, -1), waves: int = 0, stream=None, flags: int = 0,
+                     substrips: int = 0, strip_waves: int = 0, timeout_ms: int = 0) -> None:
+        """Launch column band r of nbands (asynchronous).  d_s1 / d_s2: the WHOLE
+        sequences; table: alloc_table(n_cols - 1, n2) for the band's colband_layout
+        n_cols; feed_in / feed_out: Feed buffers' addresses (raw ints, e.g. peer
+        memory from ipc_open_handle) or None at the ends."""
+        import torch
+        n1, n2 = int(d_s1.numel()), int(d_s2.numel())
+        assert table.dtype == torch.int32 and table.is_contiguous()
+        if stream is None:
+            stream = torch.cuda.current_stream(table.device)
+        b = NwColBand(feed_in, feed_out, int(tag), int(nbands), int(r), 0)
+        p = params(scheme, waves, self.device, flags, substrips, strip_waves, timeout_ms)
+        st = lib().nw_fill_colband_async(self._h, ctypes.c_void_p(d_s1.data_ptr() if n1 else 0), n1,
+                                         ctypes.c_void_p(d_s2.data_ptr() if n2 else 0), n2, ctypes.byref(p),
+                                         ctypes.byref(b), ctypes.c_void_p(table.data_ptr()), table.shape[1],
+                                         ctypes.c_void_p(stream.cuda_stream))
+        if st != NW_OK:
+            raise NwError(st, "nw_fill_colband_async")
 
     def sw_traceback(self, d_s1, d_s2, table, end, scheme=(1, -1, -1)):
         """Traceback of a device SW table (filled with mode=MODE_SW) from end = (i, j):

@@ -243,6 +243,51 @@ int nw_fill_band_async(nw_ctx *ctx, const int8_t *d_s1, int64_t n1, const int8_t
                        int64_t n2_band, const nw_params *p, const nw_band *band, int32_t *d_t,
                        int64_t pitch, void *stream);
 
+/* Column bands (multi-GPU, n1 >> n2) ------------------------------------------
+ * The reference's twin is src/mpi/mpi-vert.cpp:4-109 (+ mpi-vert-driver.cpp:35-38):
+ * rank r fills a contiguous band of columns whose column 0 is rank r-1's last
+ * column, received in COMMBUF_SIZE-row chunks while r-1 is still filling.  Here
+ * the bands are whole strips of the global table's sweep (strips of
+ * W = 64 * substrips * strip_waves columns starting at column 1): band r owns
+ * strips [strip_first, strip_first + strip_count) and its local table holds
+ * global columns [start, start + n_cols), start = strip_first * W, so local
+ * column 0 is band r-1's last column as in mpi-vert.  The first strip of band
+ * r > 0 takes that column from `feed_in` as band r-1's last strip produces it
+ * (granules {tag:32 | value:32}, one per row, nw_feed_bytes), and band r's last
+ * strip publishes its right column into `feed_out` (band r+1's feed_in, usually
+ * peer memory mapped with nw_ipc_open_handle) row block by row block.  After
+ * the fill, local column 0 of band r > 0 is written from feed_in.  Every band
+ * must use the same n1, n2 and strip shape (explicit substrips / strip_waves, or
+ * 0/0 = the tuned shape of the whole n1 x n2 table); NW mode only. */
+typedef struct nw_colband {
+    const uint64_t *feed_in;  /* NULL: first band (column 0 = the boundary i*gap) */
+    uint64_t *feed_out;       /* NULL: last band                                  */
+    uint32_t tag;             /* launch tag (> 0, the same on both sides of a feed,
+                                 new for every launch; not the value of any other
+                                 launch's tag on these buffers)                    */
+    int32_t nbands;           /* bands of the table                               */
+    int32_t r;                /* this band                                        */
+    int32_t reserved;
+} nw_colband;
+
+/* Layout of band r of nbands over an n1 x n2 table with the strip shape of `p`:
+ * its strips and the global column range of its local table (local column 0 =
+ * global column start).  Returns NW_ERR_ARG when nbands exceeds the strips. */
+int nw_colband_layout(int64_t n1, int64_t n2, int32_t nbands, int32_t r, const nw_params *p,
+                      int64_t *strip_first, int64_t *strip_count, int64_t *start, int64_t *n_cols);
+
+/* Bytes of one feed granule buffer for n2 (+1) rows, and a zeroed one of its own
+ * hipMalloc (exportable by nw_ipc_get_handle); free with nw_halo_free. */
+int64_t nw_feed_bytes(int64_t n2);
+int nw_feed_alloc(int device, int64_t n2, uint64_t **d_feed);
+
+/* Fill column band band->r: d_s1 / d_s2 the WHOLE sequences (n1 / n2); d_t the
+ * band's local table laid out like nw_table_offset's (n_cols - 1 = its "n1"),
+ * pitch >= nw_table_pitch(n_cols - 1).  Asynchronous on `stream`. */
+int nw_fill_colband_async(nw_ctx *ctx, const int8_t *d_s1, int64_t n1, const int8_t *d_s2,
+                          int64_t n2, const nw_params *p, const nw_colband *band, int32_t *d_t,
+                          int64_t pitch, void *stream);
+
 /* Cross-process device pointers (one process per GPU): export a device
  * allocation, open a peer's export.  Handles are NW_IPC_HANDLE_BYTES bytes. */
 #define NW_IPC_HANDLE_BYTES 64

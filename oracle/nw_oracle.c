@@ -16,6 +16,8 @@
  *   src/idxarray/idxarray-mt.cpp:4-70  nw_oracle_fill_idxarray   (CPU baseline "port")
  *   src/mpi/mpi-horz.cpp:4-99 +
  *   src/mpi/mpi-horz-driver.cpp:31-32  nw_oracle_band_layout / nw_oracle_fill_band
+ *   src/mpi/mpi-vert.cpp:4-109 +
+ *   src/mpi/mpi-vert-driver.cpp:35-36  nw_oracle_colband_layout / nw_oracle_fill_colband
  *   src/common/needleman-wunsch.hpp:11-16  scoring constants -> runtime parameters
  */
 #include <stdint.h>
@@ -219,6 +221,40 @@ void nw_oracle_fill_band(const int8_t *s1, int64_t n1, const int8_t *s2, int64_t
         for (int64_t j = 1; j < nCols; ++j) {
             left = ref_cell(up[j - 1], up[j], left, s1[j - 1], b, match, mismatch, gap);
             row[j] = left;
+        }
+    }
+}
+
+/* Column band layout of mpi-vert-driver.cpp:35-36 / mpi-vert.cpp:17: band r holds
+ * nCols = (n1+1)/P (+1 for r > 0: column 0 is band r-1's last column, + the
+ * remainder on the last band) columns from global column start. */
+void nw_oracle_colband_layout(int64_t n1, int P, int r, int64_t *n_cols, int64_t *start) {
+    const int64_t total = n1 + 1, base = total / P;
+    *n_cols = base + (r > 0) + (r == P - 1 ? total % P : 0);
+    *start = base * r - (r > 0);
+}
+
+/*
+ * Fill one column band (mpi-vert.cpp:4-109 semantics, without the chunked MPI
+ * pipeline) of global columns [start, start + nCols): row 0 is
+ * (j + start) * GAP (:20); column 0 is i * GAP for the first band (:26), else
+ * `left` -- band r-1's last column, n2+1 values (:54-59); cell (i, j) takes
+ * s1[start + j - 1] (:32).  t is (n2+1) x nCols, row-major.
+ */
+void nw_oracle_fill_colband(const int8_t *s1, const int8_t *s2, int64_t n2,
+                            int32_t match, int32_t mismatch, int32_t gap,
+                            int64_t start, int64_t nCols, const int32_t *left, int32_t *t) {
+    for (int64_t j = 0; j < nCols; ++j) t[j] = (int32_t)((j + start) * (int64_t)gap);
+    for (int64_t i = 0; i <= n2; ++i)
+        t[i * nCols] = left ? left[i] : (int32_t)(i * (int64_t)gap);
+    for (int64_t i = 1; i <= n2; ++i) {
+        const int8_t b = s2[i - 1];
+        int32_t *row = t + i * nCols;
+        const int32_t *up = row - nCols;
+        int32_t l = row[0];
+        for (int64_t j = 1; j < nCols; ++j) {
+            l = ref_cell(up[j - 1], up[j], l, s1[start + j - 1], b, match, mismatch, gap);
+            row[j] = l;
         }
     }
 }

@@ -60,6 +60,10 @@ def lib() -> ctypes.CDLL:
         L.nw_oracle_fill_band.argtypes = [_i8p, ctypes.c_int64, _i8p, ctypes.c_int64,
                                           ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                           ctypes.c_int, ctypes.c_int, _i32p, _i32p]
+        L.nw_oracle_colband_layout.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                                               ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
+        L.nw_oracle_fill_colband.argtypes = [_i8p, _i8p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                             ctypes.c_int32, ctypes.c_int64, ctypes.c_int64, _i32p, _i32p]
         L.nw_oracle_synth.argtypes = [ctypes.c_uint64, ctypes.c_int64, _i8p]
         L.nw_oracle_sw_fill.argtypes = [_i8p, ctypes.c_int64, _i8p, ctypes.c_int64, ctypes.c_int32,
                                         ctypes.c_int32, ctypes.c_int32, _i32p]
@@ -144,6 +148,28 @@ def fill_band(s1, s2, P, r, halo, scheme=(1, 0, -1)) -> np.ndarray:
     h = np.ascontiguousarray(halo, dtype=np.int32) if halo is not None else np.zeros(a.size + 1, np.int32)
     lib().nw_oracle_fill_band(_p(a, _i8p), a.size, _p(b, _i8p), b.size, *scheme, P, r,
                               _p(h, _i32p), _p(t, _i32p))
+    return t
+
+
+def colband_layout(n1: int, P: int, r: int):
+    """(n_cols, start) of column band r (mpi-vert-driver.cpp:35-36, mpi-vert.cpp:17)."""
+    nc, st = ctypes.c_int64(), ctypes.c_int64()
+    lib().nw_oracle_colband_layout(n1, P, r, ctypes.byref(nc), ctypes.byref(st))
+    return nc.value, st.value
+
+
+def fill_colband(s1, s2, start: int, n_cols: int, left, scheme=(1, 0, -1)) -> np.ndarray:
+    """Global columns [start, start + n_cols) given column `start` (`left`, n2+1
+    values; None for the first band) -- mpi-vert.cpp:4-109."""
+    a, b = _seq(s1), _seq(s2)
+    assert 0 <= start and start + n_cols <= a.size + 1
+    t = np.empty((b.size + 1, n_cols), dtype=np.int32)
+    lp = None
+    if left is not None:
+        left = np.ascontiguousarray(left, dtype=np.int32)
+        assert left.size == b.size + 1
+        lp = _p(left, _i32p)
+    lib().nw_oracle_fill_colband(_p(a, _i8p), _p(b, _i8p), b.size, *scheme, start, n_cols, lp, _p(t, _i32p))
     return t
 
 
