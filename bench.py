@@ -42,8 +42,9 @@ def parse():
     ap.add_argument("--band-rows", type=int, default=65536,
                     help="N>1: rows per GPU band (weak scaling; N=8 -> 512k x 512k, config 4)")
     ap.add_argument("--band-cols", type=int, default=524288, help="N>1: table columns n1")
-    ap.add_argument("--partition", choices=["rows", "cols"], default="rows",
-                    help="N>1: row bands (mpi-horz, config 4) or column bands (mpi-vert)")
+    ap.add_argument("--partition", choices=["rows", "cols"], default="cols",
+                    help="N>1: column bands (mpi-vert; default: the shorter critical path, "
+                         "DESIGN.md 'Multi-GPU') or row bands (mpi-horz, config 4's partition)")
     ap.add_argument("--col-width", type=int, default=65536,
                     help="N>1 column bands: columns per GPU (weak scaling; n1 = N x this)")
     ap.add_argument("--col-rows", type=int, default=524288, help="N>1 column bands: table rows n2")

@@ -167,7 +167,7 @@ def test_two_process_bands_shared_gpu(torch_gpu):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
-           "--share-gpu", "--band-rows", str(rows), "--band-cols", str(n1)]
+           "--share-gpu", "--partition", "rows", "--band-rows", str(rows), "--band-cols", str(n1)]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-3000:]
     line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1]

@@ -10,8 +10,9 @@ src/mpi/mpi-horz-driver.cpp:31-32, mpi-horz.cpp:16-40.
 CPU (-m "not gpu"): the golden files decode consistently, agree with
 synth_scores.json, and the 64k file matches the oracle recomputed here.
 GPU (-m gpu): config 3 (262144^2, 275 GB table, one MI355X) under both schemes,
-the 64k/128k squares, and config 4's row-band geometry (524288 columns in 8
-bands of 4096 rows) through LocalBands.
+the 64k/128k squares, and a 524288 x 32767 table split as config 4 is on 8 GPUs:
+8 row bands of 4096 rows (LocalBands) and 8 column bands of 256 strips
+(LocalColBands, mpi-vert.cpp:4-109).
 """
 import json
 import os
@@ -81,15 +82,16 @@ def ctx(torch):
     c.close()
 
 
-def row_checksums(torch, tab, rows, n_cols, chunk=256):
+def row_checksums(torch, tab, rows, n_cols, chunk=256, col_first=0, col_base=0):
     """(sum, column-weighted sum) per row mod 2^64 (oracle.row_checksums) on the device,
     `rows` = the table rows to check, in chunks (a few hundred MB of temporaries next
-    to a 275 GB table)."""
-    w = torch.arange(1, n_cols + 1, dtype=torch.int64, device=tab.device)
+    to a 275 GB table).  Columns col_first .. n_cols-1 of `tab`, local column k being
+    global column col_base + k (a column band's part of the sums)."""
+    w = torch.arange(col_base + col_first + 1, col_base + n_cols + 1, dtype=torch.int64, device=tab.device)
     rs, rw = [], []
     for r0 in range(0, rows, chunk):
         r1 = min(rows, r0 + chunk)
-        t64 = tab[r0:r1, :n_cols].to(torch.int64)
+        t64 = tab[r0:r1, col_first:n_cols].to(torch.int64)
         rs.append(t64.sum(dim=1).cpu())
         rw.append((t64 * w).sum(dim=1).cpu())
         del t64
@@ -162,6 +164,40 @@ def test_config4_band_geometry(torch):
             np.testing.assert_array_equal(tab[:rows, n1].cpu().numpy(), g["last_col"][start:start + rows])
         rows, _ = lb.layout[-1]
         np.testing.assert_array_equal(lb.tables[-1][rows - 1, :n1 + 1].cpu().numpy(), g["last_row"])
+    finally:
+        lb.close()
+        del lb
+        torch.cuda.empty_cache()
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+def test_config4_colband_geometry(torch):
+    """The same 524288 x 32767 table as 8 column bands (mpi-vert partition, the bench's
+    default multi-GPU one), concurrently on one device through the in-kernel feed
+    hand-off: every row's checksums assembled over the bands (each band's shared left
+    column counted once), the last row and last column against the golden rows."""
+    import nw_bands
+    n1, n2, P = 524288, 32767, 8
+    g = big_rows(n1, n2, (1, 0, -1))
+    torch.cuda.empty_cache()
+    lb = nw_bands.LocalColBands(n1, n2, P)
+    try:
+        score = lb.fill(torch.from_numpy(nwhip.synth(1, n1)).cuda(),
+                        torch.from_numpy(nwhip.synth(2, n2)).cuda())
+        assert score == g["score"]
+        rs_all = np.zeros(n2 + 1, np.uint64)
+        rw_all = np.zeros(n2 + 1, np.uint64)
+        for r, (sf, sc, start, ncols) in enumerate(lb.layout):
+            tab = lb.tables[r]
+            rs, rw = row_checksums(torch, tab, n2 + 1, ncols, col_first=1 if r else 0, col_base=start)
+            rs_all += rs
+            rw_all += rw
+            np.testing.assert_array_equal(tab[n2, :ncols].cpu().numpy(), g["last_row"][start:start + ncols],
+                                          err_msg=f"band {r}")
+        np.testing.assert_array_equal(rs_all, g["row_sum"])
+        np.testing.assert_array_equal(rw_all, g["row_wsum"])
+        np.testing.assert_array_equal(lb.tables[-1][:n2 + 1, lb.layout[-1][3] - 1].cpu().numpy(), g["last_col"])
     finally:
         lb.close()
         del lb
