@@ -220,7 +220,7 @@ int nw_ctx_create(int device, nw_ctx **out) {
     c->device = device;
     c->cus = prop.multiProcessorCount;
     if (hipMalloc(&c->ctrl, 32) != hipSuccess || hipMemset(c->ctrl, 0, 32) != hipSuccess ||
-        hipMalloc(&c->meta, nw::kMetaBytes) != hipSuccess ||
+        hipMalloc(&c->meta, nw::kMetaBytes) != hipSuccess || hipMemset(c->meta, 0, nw::kMetaBytes) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
         nw_ctx_destroy(c);
         return NW_ERR_HIP;

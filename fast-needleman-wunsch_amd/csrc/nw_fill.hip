@@ -1248,40 +1248,51 @@ __global__ __launch_bounds__((64 * Lay<C, NC>::kWaves)) void nw_fill_strips(Fill
     }
 }
 
-// Column-character map of a launch (one workgroup): which byte values occur in
-// s1, in increasing order -> charmap[c] = index (0xFF: absent), *nprof = how
-// many distinct characters s1 holds.
-__global__ __launch_bounds__(1024) void nw_charmap(const uint8_t *__restrict__ s1, int64_t n1,
-                                                   uint8_t *__restrict__ charmap,
-                                                   uint32_t *__restrict__ nprof) {
-    __shared__ uint32_t present[8];
-    __shared__ uint32_t before[8];
-    if (threadIdx.x < 8) present[threadIdx.x] = 0;
+// Column-character map of a launch, in two kernels: nw_charmap_scan (a grid of
+// workgroups, each byte of s1 read once, coalesced) ORs which byte values occur
+// in s1 into present[8]; nw_charmap_finish (one workgroup) turns that into
+// charmap[c] = index of c among them in increasing order (0xFF: absent) and
+// *nprof = how many distinct characters s1 holds, then zeroes present[] for the
+// next launch (it starts zeroed: nw_ctx_create).
+constexpr int kScanBytesPerWG = 8192;
+__global__ __launch_bounds__(256) void nw_charmap_scan(const uint8_t *__restrict__ s1, int64_t n1,
+                                                        uint32_t *__restrict__ present) {
+    __shared__ uint32_t loc[8];
+    if (threadIdx.x < 8) loc[threadIdx.x] = 0;
     __syncthreads();
     uint32_t mine[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int64_t i = threadIdx.x; i < n1; i += blockDim.x) {
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n1; i += stride) {
         const uint32_t c = s1[i];
-        mine[c >> 5] |= 1u << (c & 31);
+#pragma unroll
+        for (int w = 0; w < 8; ++w) mine[w] |= (c >> 5) == (uint32_t)w ? 1u << (c & 31) : 0u;
     }
 #pragma unroll
     for (int w = 0; w < 8; ++w)
-        if (mine[w]) atomicOr(&present[w], mine[w]);
+        if (mine[w]) atomicOr(&loc[w], mine[w]);
+    __syncthreads();
+    if (threadIdx.x < 8 && loc[threadIdx.x]) atomicOr(present + threadIdx.x, loc[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(256) void nw_charmap_finish(uint32_t *__restrict__ present,
+                                                          uint8_t *__restrict__ charmap,
+                                                          uint32_t *__restrict__ nprof) {
+    __shared__ uint32_t pw[8], before[8];
+    if (threadIdx.x < 8) pw[threadIdx.x] = present[threadIdx.x];
     __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t acc = 0;
         for (int w = 0; w < 8; ++w) {
             before[w] = acc;
-            acc += (uint32_t)__builtin_popcount(present[w]);
+            acc += (uint32_t)__builtin_popcount(pw[w]);
         }
         *nprof = acc;
     }
     __syncthreads();
-    if (threadIdx.x < 256) {
-        const uint32_t c = threadIdx.x, w = c >> 5, bit = 1u << (c & 31);
-        const uint32_t idx = before[w] + (uint32_t)__builtin_popcount(present[w] & (bit - 1u));
-        const bool here = (present[w] & bit) != 0u;
-        charmap[c] = here ? (uint8_t)min(idx, 255u) : (uint8_t)0xFF;
-    }
+    const uint32_t c = threadIdx.x, w = c >> 5, bit = 1u << (c & 31);
+    const uint32_t idx = before[w] + (uint32_t)__builtin_popcount(pw[w] & (bit - 1u));
+    charmap[c] = (pw[w] & bit) != 0u ? (uint8_t)min(idx, 255u) : (uint8_t)0xFF;
+    if (threadIdx.x < 8) present[threadIdx.x] = 0u;
 }
 
 // rowpack16[idx] = B[x .. x+15] (16 bytes), x = idx - kQOff, B[y] = s2[row0 + y - 1]
@@ -1335,8 +1346,10 @@ int launch_rowpack(const uint8_t *d_s1, int64_t n1, const uint8_t *d_s2, int64_t
                    int32_t perm, uint8_t *meta, void *d_q, int64_t qlen, void *stream) {
     uint8_t *charmap = meta;
     uint32_t *nprof = (uint32_t *)(meta + 256);
-    hipLaunchKernelGGL(nw_charmap, dim3(1), dim3(1024), 0, (hipStream_t)stream, d_s1, n1, charmap,
-                       nprof);
+    uint32_t *present = (uint32_t *)(meta + 272);
+    const int64_t g = std::min<int64_t>(256, std::max<int64_t>(1, (n1 + kScanBytesPerWG - 1) / kScanBytesPerWG));
+    hipLaunchKernelGGL(nw_charmap_scan, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, d_s1, n1, present);
+    hipLaunchKernelGGL(nw_charmap_finish, dim3(1), dim3(256), 0, (hipStream_t)stream, present, charmap, nprof);
     const int bs = 256;
     const int64_t nb = (qlen + bs - 1) / bs;
     hipLaunchKernelGGL(nw_rowpack, dim3((unsigned)nb), dim3(bs), 0, (hipStream_t)stream, d_s2, n2,

@@ -12,7 +12,7 @@ constexpr int kScratchWords = kWave * kWave + 2 * kWave;  // per workgroup (16.5
 constexpr int kMaxSub = 4;        // max columns per lane (strip = 64 * C columns)
 constexpr int kTraceWords = 24;    // debug trace words per strip (nw_debug_trace_words)
 constexpr uint32_t kMaxPerm = 7;  // distinct column characters the v_perm score tables cover
-constexpr int kMetaBytes = 256 + 16;  // charmap[256], nprof (+ pad)
+constexpr int kMetaBytes = 256 + 16 + 32;  // charmap[256], nprof (+ pad), present[8] (zero between launches)
 
 // Everything one launch of the strip-sweep kernel needs.  Plain POD, passed by
 // value as the kernel argument.

@@ -12,7 +12,7 @@ import pytest
 
 import nwhip
 import oracle
-from conftest import GOLDEN, PKG, bdna_path
+from conftest import GOLDEN, PKG, ROOT, bdna_path
 
 pytestmark = pytest.mark.gpu
 SCHEMES = oracle.SCHEMES
@@ -324,3 +324,21 @@ def test_dropin_driver_cli(golden, drv, name, want):
     lines = out.stdout.strip().split("\n")
     assert len(lines) == 2 and lines[0].isdigit()          # "<ms>" (driver.cpp:33)
     assert lines[1] == f"Score: {want}"                      # driver.cpp:35
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,want", [("small", 3), ("t", 7), ("debug", 27), ("smid", 5839)])
+def test_reference_driver_links_the_dropin(golden, name, want):
+    """The reference's OWN, unmodified driver.cpp + helper.cpp (compiled in the build
+    container by oracle/Makefile ref-dropin into oracle/_ref/ref_driver_hip) linked
+    against the drop-in TU: the genuine caller of the plugin symbol runs the HIP fill."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "ref_driver_hip")
+    if not os.path.exists(exe):
+        pytest.skip("oracle/_ref/ref_driver_hip not built (needs the reference tree at build time)")
+    e = golden["pairs"][name]
+    out = subprocess.run([exe, bdna_path(e["argv1"]), bdna_path(e["argv2"])], capture_output=True,
+                         text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    lines = out.stdout.strip().split("\n")
+    assert len(lines) == 2 and lines[0].isdigit()
+    assert lines[1] == f"Score: {want}"
