@@ -1017,15 +1017,22 @@ __device__ __forceinline__ void store_strip_grp(const FillArgs &A, char *__restr
     const uint32_t ug = A.sw ? 0u : (uint32_t)A.gap;  // SW rings hold t itself
     // ring byte offset (within the ring) of column a = 32h + 4cq + k of row f0 + ro,
     // and kc = GAP * (row + column) of it (the ring holds w = t - GAP*(i+j))
+    // The right half (columns 32..63) of a row completes 32 steps after the left
+    // half, so a batch pairs the left halves of rows f .. f+BATCH-1 with the right
+    // halves of rows f-32 .. f-32+BATCH-1: both are complete from step
+    // f + BATCH - 1 + 32 on, and a ring slot (step x: column a of row x - a) is
+    // free once the left halves of rows <= x and the right halves of rows <= x - 32
+    // are read -- 32 steps earlier than with whole rows.
+    constexpr int32_t kLagH = 32;
     uint32_t pa[2][4], kc[2][4];
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint32_t a = (uint32_t)(32 * h + 4 * cq + k);
-            const uint32_t st = (uint32_t)(f0 + ro) + a;
+            const uint32_t st = (uint32_t)(f0 + ro) + a + (h ? (uint32_t)(kR - kLagH) : 0u);  // (mod kR)
             pa[h][k] = (((st >> 2) * 1024u) & kMask) + grp_pos(a) * 16u + (st & 3u) * 4u;
-            kc[h][k] = ug * (uint32_t)(f0 + ro) + ug * (uint32_t)(c0 + a);
+            kc[h][k] = ug * (uint32_t)(f0 + ro - kLagH * h) + ug * (uint32_t)(c0 + a);
         }
     // the last strip may overhang the pitch: store only 16-byte pieces wholly inside the row
     bool col_ok[2];
@@ -1052,70 +1059,84 @@ __device__ __forceinline__ void store_strip_grp(const FillArgs &A, char *__restr
     const bool trace = A.trace != nullptr && j == 0 && q == 0;
     uint64_t tw = 0, ts = 0;
     int32_t avail = 0;
-    // rows f .. f+BATCH-1 complete in the ring (bounded wait)
+    // batch f complete in the ring: left halves of rows < min(f + BATCH, nrows)
+    // (step + 32) and right halves of rows < min(f - 32 + BATCH, nrows) (step + 64);
+    // `avail` = steps known written (bounded wait)
     auto wait_rows = [&](int32_t f) {
-        const int32_t want = min(f + BATCH, nrows);
+        const int32_t want = max(min(f + BATCH, nrows) + 31, min(f - kLagH + BATCH, nrows) + 63);
         if (avail < want) {
             const uint64_t t0 = trace ? __builtin_amdgcn_s_memtime() : 0;
             int32_t sa = __builtin_amdgcn_readfirstlane(ctr_load(ctr));
-            if (sa != kDone && sa - 63 < want) sa = wait_counter(ctr, want + 63, A.ctrl, 8, A.timeout_ticks);
-            avail = (sa == kDone || sa == kDead) ? nrows : min(sa - 63, nrows);
+            if (sa != kDone && sa < want) sa = wait_counter(ctr, want, A.ctrl, 8, A.timeout_ticks);
+            avail = (sa == kDone || sa == kDead) ? INT32_MAX : sa;
             lds_order();
             if (bcol) bnd0 = *bnd0p;
             if (trace) tw += __builtin_amdgcn_s_memtime() - t0;
         }
     };
-    // the next batch from the ring into v (the LDS reads are only issued here;
-    // the stores of the previous batch go out while they are in flight)
+    // the next batch from the ring into v, raw (only the LDS reads are issued
+    // here: nothing waits for them until the batch's own stores, one pipeline
+    // stage later, so the stores of the previous batch go out while they are in
+    // flight)
     auto read_batch = [&](u32x4 (&v)[NU][2]) {
 #pragma unroll
         for (int g = 0; g < NU; ++g)
 #pragma unroll
             for (int h = 0; h < 2; ++h)
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const uint32_t x = *(const uint32_t *)(lds + ring0 + ((pa[h][k] + g * 2048u) & kMask));
-                    v[g][h][k] = x + kc[h][k] + ug * (uint32_t)(8 * g);
-                }
+                for (int k = 0; k < 4; ++k)
+                    v[g][h][k] = *(const uint32_t *)(lds + ring0 + ((pa[h][k] + g * 2048u) & kMask));
 #pragma unroll
         for (int h = 0; h < 2; ++h)
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                pa[h][k] = (pa[h][k] + (uint32_t)(NS * BATCH / 4) * 1024u) & kMask;
-                kc[h][k] += ug * (uint32_t)(NS * BATCH);
-            }
+            for (int k = 0; k < 4; ++k) pa[h][k] = (pa[h][k] + (uint32_t)(NS * BATCH / 4) * 1024u) & kMask;
     };
-    // stores of batch f (v from read_batch); its ring slots are released first
-    auto store_batch = [&](int32_t f, const u32x4 (&v)[NU][2]) {
-        // (in-order LDS: this counter store executes after the batch's reads)
+    // stores of batch f (v from read_batch).  First the ring slots of every
+    // batch read so far are released: `fr`, the last batch read (f, or f + D when
+    // the next batch is already in registers); in-order LDS makes this counter
+    // store execute after those reads.
+    auto store_batch = [&](int32_t f, u32x4 (&v)[NU][2], int32_t fr) {
         lds_order();
-        ctr_store(mine, f + NS * BATCH);
+        ctr_store(mine, fr + NS * BATCH);
+        // t = w + GAP*(i+j): kc holds it for row f0 + ro; batch f adds GAP*(f - f0 + 8g)
+        const uint32_t kf = ug * (uint32_t)(f - f0);
+#pragma unroll
+        for (int g = 0; g < NU; ++g)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) v[g][h][k] += kc[h][k] + kf + ug * (uint32_t)(8 * g);
+        // row of unit g of half h: f + 8g + ro - 32h
         if (A.sw) {
 #pragma unroll
-            for (int g = 0; g < NU; ++g) {
-                const bool rok = f + g * 8 + ro < nrows;
+            for (int g = 0; g < NU; ++g)
 #pragma unroll
-                for (int h = 0; h < 2; ++h)
+                for (int h = 0; h < 2; ++h) {
+                    const int32_t r = f + g * 8 + ro - kLagH * h;
+                    const bool rok = r >= 0 && r < nrows;
 #pragma unroll
                     for (int k = 0; k < 4; ++k)
                         vmax = max(vmax, (rok && ((cval >> (4 * h + k)) & 1u)) ? (int32_t)v[g][h][k] : 0);
-            }
+                }
         }
         const uint64_t t0 = trace ? __builtin_amdgcn_s_memtime() : 0;
         char *rp = rowp + (int64_t)(f - f0) * rowb;
-        if (min(f + BATCH, nrows) - f == BATCH) {
+        if (f >= kLagH && f + BATCH <= nrows) {
 #pragma unroll
             for (int g = 0; g < NU; ++g)
 #pragma unroll
                 for (int h = 0; h < 2; ++h)
-                    if (col_ok[h]) *(u32x4 *)(rp + (int64_t)g * 8 * rowb + voff + h * 128) = v[g][h];
+                    if (col_ok[h])
+                        *(u32x4 *)(rp + (int64_t)(g * 8 - kLagH * h) * rowb + voff + h * 128) = v[g][h];
         } else {
 #pragma unroll
             for (int g = 0; g < NU; ++g)
 #pragma unroll
-                for (int h = 0; h < 2; ++h)
-                    if (col_ok[h] && f + g * 8 + ro < nrows)
-                        *(u32x4 *)(rp + (int64_t)g * 8 * rowb + voff + h * 128) = v[g][h];
+                for (int h = 0; h < 2; ++h) {
+                    const int32_t r = f + g * 8 + ro - kLagH * h;
+                    if (col_ok[h] && r >= 0 && r < nrows)
+                        *(u32x4 *)(rp + (int64_t)(g * 8 - kLagH * h) * rowb + voff + h * 128) = v[g][h];
+                }
         }
         if (bcol) {
 #pragma unroll
@@ -1128,38 +1149,40 @@ __device__ __forceinline__ void store_strip_grp(const FillArgs &A, char *__restr
         if (trace) ts += __builtin_amdgcn_s_memtime() - t0;
     };
     constexpr int32_t D = NS * BATCH;
-    // Deadlock freedom of the pipeline: before storing batch f a store wave
-    // waits for batch f + D, i.e. for step f + D + BATCH - 1 + 63, while the
-    // rows it has released stop at f; the compute wave writes that step only
-    // once rows <= step + kChk - kR are read.
-    static_assert(D + BATCH - 1 + 63 + L::kChk - kR <= 0, "store pipeline lookahead exceeds the ring");
+    // Deadlock freedom of the pipeline: a store wave waits for batch f + D, i.e.
+    // for step f + D + BATCH - 1 + 32, having released the slots of the steps
+    // below f + D (at the stores of batch f - D, after reading batch f); the
+    // compute wave writes that step once slots <= step + kChk - kR are free.
+    static_assert(BATCH - 1 + 32 + L::kChk - kR <= 0, "store pipeline lookahead exceeds the ring");
+    // batches run to f < nrows + 32: the right halves of the last 32 rows
+    const int32_t fend = nrows + kLagH;
     if (A.flags & 4) {  // debug: drain the ring without reading it
-        for (int32_t f = f0; f < nrows; f += D) {
+        for (int32_t f = f0; f < fend; f += D) {
             wait_rows(f);
             lds_order();
             ctr_store(mine, f + D);
         }
-    } else if (f0 < nrows) {
+    } else if (f0 < fend) {
         // software pipeline over two register sets: batch f + D is read while
         // batch f is stored
         u32x4 va[NU][2], vb[NU][2];
         wait_rows(f0);
         read_batch(va);
         for (int32_t f = f0;; f += 2 * D) {
-            if (f + D >= nrows) {
-                store_batch(f, va);
+            if (f + D >= fend) {
+                store_batch(f, va, f);
                 break;
             }
             wait_rows(f + D);
             read_batch(vb);
-            store_batch(f, va);
-            if (f + 2 * D >= nrows) {
-                store_batch(f + D, vb);
+            store_batch(f, va, f + D);
+            if (f + 2 * D >= fend) {
+                store_batch(f + D, vb, f + D);
                 break;
             }
             wait_rows(f + 2 * D);
             read_batch(va);
-            store_batch(f + D, vb);
+            store_batch(f + D, vb, f + 2 * D);
         }
     }
     ctr_store(mine, kDone);
@@ -1171,7 +1194,7 @@ __device__ __forceinline__ void store_strip_grp(const FillArgs &A, char *__restr
         trw[18] = ts;
     }
     // Row band: hand this ring's 64 columns of the last row to the next band (see store_strip)
-    if (A.halo_out != nullptr && ((nrows - 1) / BATCH) % NS == q && ctrl_load(A.ctrl + 1) == 0u) {
+    if (A.halo_out != nullptr && ((nrows - 1 + kLagH) / BATCH) % NS == q && ctrl_load(A.ctrl + 1) == 0u) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         const int32_t *last = A.table + A.n2 * A.pitch;
