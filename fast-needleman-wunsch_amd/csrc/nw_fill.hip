@@ -323,13 +323,13 @@ __device__ __forceinline__ int32_t diag_plus_sub(uint32_t w, uint32_t apk, int32
                                                  int32_t msp, int32_t mmp) {
     int32_t d;
     if constexpr (MODE == SUB_PERM || MODE == SUB_PERM_SW) {
-        // w = v_perm result: byte QB = s'(a_k, row of step QB)
-        asm("v_add_u32_sdwa %0, %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD "
-            "src0_sel:DWORD src1_sel:BYTE_%c3"
-            : "=v"(d)
-            : "v"(diag), "v"(w), "i"(QB));
+        // w = v_perm result: byte QB = s'(a_k, row of step QB).  Written in C++ so
+        // that the compiler forms the v_add_u32_sdwa (sext BYTE_QB) itself and
+        // schedules it: as inline asm it was opaque to the scheduler (C = 4: 99 ->
+        // 91 cycles per step, C = 2: 71 -> 64, C = 1: 53 -> 49).
+        d = diag + (int32_t)(int8_t)(uint8_t)(w >> (8 * QB));
     } else if constexpr (MODE == SUB_UNIT) {
-        asm volatile(
+        asm(
             "v_cmp_eq_u32_sdwa vcc, %1, %2 src0_sel:BYTE_%c4 src1_sel:BYTE_%c5\n\t"
             "v_addc_co_u32_e32 %0, vcc, %3, %6, vcc"
             : "=v"(d)
@@ -337,7 +337,7 @@ __device__ __forceinline__ int32_t diag_plus_sub(uint32_t w, uint32_t apk, int32
             : "vcc");
     } else {
         int32_t sc;
-        asm volatile(
+        asm(
             "v_cmp_eq_u32_sdwa vcc, %1, %2 src0_sel:BYTE_%c5 src1_sel:BYTE_%c6\n\t"
             "v_cndmask_b32_e32 %0, %3, %4, vcc"
             : "=v"(sc)
@@ -489,8 +489,12 @@ __device__ __forceinline__ void run_iter(char *__restrict__ lds, int it, const u
             constexpr int q = decltype(qc)::value;
             constexpr int u = 4 * g + q;
             const int32_t lf = q == 0 ? fcur.x : q == 1 ? fcur.y : q == 2 ? fcur.z : fcur.w;
+#ifdef NW_EXP_NODPP  // timing experiment only (wrong results): no cross-lane shift
+            int32_t left = S.u[C - 1] + lf;
+#else
             int32_t left = __builtin_amdgcn_update_dpp(lf, S.u[C - 1], 0x138 /*wave_shr:1*/,
                                                        0xF, 0xF, false);
+#endif
             int32_t diag = S.dg;
             S.dg = left;
             bool act = true;
@@ -524,7 +528,11 @@ __device__ __forceinline__ void run_iter(char *__restrict__ lds, int it, const u
                     set_comp<C>(tv, k, x);
                 }
             });
+#ifdef NW_EXP_NORING  // timing experiment only (wrong results): no ring writes
+            if constexpr (false) {
+#else
             if constexpr (!L::kGrp) {
+#endif
                 *(VT *)(ringw + u * L::kSlot) = tv;  // ring slot 64*HALF + u
             } else if constexpr ((u & 3) == 3) {
                 // group 16*HALF + u/4: this lane's record of steps u-3 .. u
