@@ -603,8 +603,11 @@ int nw_sw_traceback(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *d_s
                                 p->gap, end_i, end_j, c->ops, (int64_t)need, c->swinfo, nullptr) != hipSuccess)
         return NW_ERR_HIP;
     NW_HIP_TRY(hipEventRecord(c->ev1, nullptr));
-    int64_t info[4];
+    int64_t info[8];
     NW_HIP_TRY(hipMemcpy(info, c->swinfo, sizeof info, hipMemcpyDeviceToHost));
+    if (std::getenv("NW_TB_DEBUG"))  // traceback phase timers (s_memrealtime ticks)
+        std::fprintf(stderr, "nw_sw_traceback: windows %lld, load %.3f ms, classify %.3f ms, walk %.3f ms\n",
+                     (long long)info[7], info[4] * 1e-5, info[5] * 1e-5, info[6] * 1e-5);
     float ms = 0.f;
     NW_HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
     std::memset(out, 0, sizeof *out);

@@ -81,13 +81,18 @@ int launch_sw_locate(const int32_t *table, int64_t pitch, int64_t n1, int64_t n2
 // is staged in LDS a window at a time -- rows [i0, i] x columns [j0, j], at most
 // (kWin+1)^2 int32, every thread issuing all its loads before it waits -- with
 // the window's characters; all threads then classify every cell of the window
-// (the move the walk would take there: diag if t == t[i-1][j-1] + s, else up if
-// t == t[i-1][j] + GAP, else left, or "stop" where t == 0), and thread 0 follows
-// the codes -- one LDS byte per step -- writing one op per step, until it stops or
-// reaches the window's top row / left column, where the next window is staged.
+// with the move the walk takes there, stored as the LDS index step of that move
+// (diag: W+1, if t == t[i-1][j-1] + s; else up: W, if t == t[i-1][j] + GAP; else
+// left: 1), or a stop code: t == 0 (or row / column 0 of the table), the window's
+// own top row / left column (the walk continues in the next window), or "no
+// move matches" (not a Smith-Waterman table).  Thread 0 then follows the codes --
+// per step one dependent LDS byte read, its op byte into an LDS buffer -- and all
+// threads copy the window's ops out together.
 constexpr int kWin = 127;                       // (kWin+1)^2 int32 = 64 KB of LDS
 constexpr int kTbThreads = 1024;
 constexpr int kTbPer = ((kWin + 1) * (kWin + 1) + kTbThreads - 1) / kTbThreads;  // loads per thread
+constexpr uint8_t kMvLeft = 1, kMvUp = kWin + 1, kMvDiag = kWin + 2;  // index steps (W = kWin + 1)
+constexpr uint8_t kStop = 0, kEdge = 200, kBad = 255;
 __global__ __launch_bounds__(kTbThreads) void nw_sw_traceback(
     const int32_t *__restrict__ table, int64_t pitch, const uint8_t *__restrict__ s1,
     const uint8_t *__restrict__ s2, int32_t match, int32_t mismatch, int32_t gap, int64_t end_i, int64_t end_j,
@@ -95,19 +100,25 @@ __global__ __launch_bounds__(kTbThreads) void nw_sw_traceback(
     constexpr int W = kWin + 1;
     __shared__ int32_t win[W * W];
     __shared__ uint8_t code[W * W];
+    __shared__ uint16_t cc2[W * W];
+    __shared__ uint16_t ob[W / 2 + 2];  // the window's moves, 4 per entry (2 bits each | count << 8)
     __shared__ uint8_t c1[W], c2[W];
-    __shared__ int64_t st[4];  // i, j, steps, status (done flag in the sign of i)
+    __shared__ int64_t st[5];  // i, j, steps, status (done flag in the sign of i), moves this window
     const int tid = threadIdx.x;
     if (tid == 0) {
         st[0] = end_i;
         st[1] = end_j;
         st[2] = 0;
         st[3] = 0;
+        st[4] = 0;
     }
     __syncthreads();
+    uint64_t tl = 0, tc = 0, tw = 0, nwin = 0;  // (thread 0) ticks loading / classifying / walking
     for (;;) {
         const int64_t i = st[0], j = st[1];
         if (i <= 0 || j <= 0 || st[3] != 0) break;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        ++nwin;
         const int64_t i0 = i > kWin ? i - kWin : 0, j0 = j > kWin ? j - kWin : 0;
         const int rows = (int)(i - i0 + 1), cols = (int)(j - j0 + 1);
         int32_t v[kTbPer];
@@ -126,47 +137,108 @@ __global__ __launch_bounds__(kTbThreads) void nw_sw_traceback(
             c2[tid] = (tid >= 1 && tid < rows) ? s2[i0 + tid - 1] : 0;
         }
         __syncthreads();
-        for (int e = tid; e < W * W; e += kTbThreads) {
+        const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+        #pragma unroll
+        for (int kk = 0; kk < kTbPer; ++kk) {
+            const int e = tid + kk * kTbThreads;
             const int r = e / W, c = e % W;
-            uint8_t cd = 3;
-            if (r >= 1 && c >= 1 && r < rows && c < cols) {
+            uint8_t cd = kStop;
+            if (r >= rows || c >= cols) {
+                cd = kStop;  // (never reached: the walk starts at the bottom-right cell)
+            } else if (r == 0 || c == 0) {
+                cd = (i0 + r == 0 || j0 + c == 0) ? kStop : kEdge;
+            } else {
                 const int32_t t = win[e];
                 if (t > 0) {
                     const int32_t sc = c1[c] == c2[r] ? match : mismatch;
-                    cd = t == win[e - W - 1] + sc ? 0 : t == win[e - W] + gap ? 1 : t == win[e - 1] + gap ? 2 : 4;
+                    cd = t == win[e - W - 1] + sc ? kMvDiag
+                         : t == win[e - W] + gap  ? kMvUp
+                         : t == win[e - 1] + gap  ? kMvLeft
+                                                  : kBad;
                 }
             }
             code[e] = cd;
         }
         __syncthreads();
-        if (tid == 0) {
-            int r = rows - 1, c = cols - 1;
-            int64_t steps = st[2];
-            bool done = false;
-            while (r > 0 && c > 0) {
-                const uint8_t cd = code[r * W + c];
-                if (cd == 3) {
-                    done = true;
-                    break;
-                }
-                if (cd == 4) {
-                    st[3] = 2;  // not a Smith-Waterman table
-                    break;
-                }
-                if (steps >= ops_cap) {
-                    st[3] = 1;
-                    break;
-                }
-                ops[steps++] = cd;
-                r -= cd != 2;
-                c -= cd != 1;
+        // Multi-step codes by doubling, so that the walk below takes 4 moves per
+        // dependent LDS read: a k-step code holds the moves from a cell (2 bits
+        // each: 0 diag, 1 up, 2 left), their count and their total index step.
+        //   c2 (uint16): moves 0-3 | count 4-5 | step 6-14
+        //   c4 (uint32, in win's place -- no longer needed): moves 0-7 | count 8-10 | step 16-31
+        auto mv1 = [](uint8_t d) -> uint32_t { return d == kMvDiag ? 0u : d == kMvUp ? 1u : 2u; };
+        auto is_mv = [](uint8_t d) { return d == kMvDiag || d == kMvUp || d == kMvLeft; };
+        #pragma unroll
+        for (int kk = 0; kk < kTbPer; ++kk) {
+            const int e = tid + kk * kTbThreads;
+            const uint8_t a = code[e];
+            uint32_t w = 0;
+            if (is_mv(a)) {
+                const uint8_t b = code[e - a];
+                w = is_mv(b) ? (mv1(a) | (mv1(b) << 2) | (2u << 4) | ((uint32_t)(a + b) << 6))
+                             : (mv1(a) | (1u << 4) | ((uint32_t)a << 6));
             }
-            if (!done && (i0 + r == 0 || j0 + c == 0)) done = true;  // row / column 0: t == 0
-            st[0] = done ? -(i0 + r) - 1 : i0 + r;
-            st[1] = j0 + c;
-            st[2] = steps;
+            cc2[e] = (uint16_t)w;
         }
         __syncthreads();
+        uint32_t *c4 = (uint32_t *)win;
+        #pragma unroll
+        for (int kk = 0; kk < kTbPer; ++kk) {
+            const int e = tid + kk * kTbThreads;
+            const uint32_t a = cc2[e];
+            const uint32_t na = (a >> 4) & 3u, da = a >> 6;
+            uint32_t w = (a & 15u) | (na << 8) | (da << 16);
+            if (na == 2) {
+                const uint32_t b = cc2[e - (int)da];
+                const uint32_t nb = (b >> 4) & 3u, db = b >> 6;
+                w = (a & 15u) | ((b & 15u) << 4) | ((na + nb) << 8) | ((da + db) << 16);
+            }
+            c4[e] = w;
+        }
+        __syncthreads();
+        const uint64_t t2 = __builtin_amdgcn_s_memrealtime();
+        if (tid == 0) {
+            int idx = (rows - 1) * W + (cols - 1);
+            int k = 0, q = 0;
+            for (;;) {
+                const uint32_t w = c4[idx];
+                const int n = (int)((w >> 8) & 7u);
+                if (n == 0) break;
+                ob[q++] = (uint16_t)(w & 0x7FFu);
+                k += n;
+                idx -= (int)(w >> 16);
+                if (n < 4) break;
+            }
+            const uint8_t d = code[idx];  // where the walk stopped: kStop, kEdge or kBad
+            const int r = idx / W, c = idx % W;
+            const int64_t steps = st[2];
+            if (d == kBad) {
+                st[3] = 2;  // not a Smith-Waterman table
+            } else if (steps + k > ops_cap) {
+                st[3] = 1;
+            } else {
+                st[0] = d == kStop ? -(i0 + r) - 1 : i0 + r;  // (kEdge: next window from here)
+                st[1] = j0 + c;
+            }
+            st[4] = k;
+        }
+        __syncthreads();
+        {
+            const int k = (int)st[4];
+            const int64_t steps = st[2];
+            if (st[3] == 0)
+                for (int e = tid; 4 * e < k; e += kTbThreads) {
+                    const uint32_t w = ob[e];
+                    const int n = (int)(w >> 8);
+                    for (int m = 0; m < n; ++m) ops[steps + 4 * e + m] = (uint8_t)((w >> (2 * m)) & 3u);
+                }
+        }
+        __syncthreads();
+        if (tid == 0 && st[3] == 0) st[2] += st[4];
+        __syncthreads();
+        const uint64_t t3 = __builtin_amdgcn_s_memrealtime();
+        tl += t1 - t0;
+        tc += t2 - t1;
+        tw += t3 - t2;
         if (st[0] < 0) break;
     }
     __syncthreads();
@@ -175,6 +247,10 @@ __global__ __launch_bounds__(kTbThreads) void nw_sw_traceback(
         info[1] = st[0] < 0 ? -st[0] - 1 : st[0];
         info[2] = st[1];
         info[3] = st[3];
+        info[4] = (int64_t)tl;  // (diagnostics: s_memrealtime ticks, 100 MHz)
+        info[5] = (int64_t)tc;
+        info[6] = (int64_t)tw;
+        info[7] = (int64_t)nwin;
     }
 }
 
