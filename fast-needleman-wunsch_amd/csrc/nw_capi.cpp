@@ -454,6 +454,15 @@ void nw_band_layout(int64_t n2, int32_t nbands, int32_t r, int64_t *n_rows, int6
     if (start) *start = st;
 }
 
+// A halo / feed buffer: its own allocation (so that HIP IPC exports exactly it),
+// fine-grained -- the producing kernel on ANOTHER GPU writes it over xGMI with
+// system-scope stores while this GPU's kernel polls it with system-scope loads,
+// and system-scope coherence between agents is what fine-grained memory gives
+// (coarse-grained memory is only coherent at agent scope).
+static hipError_t alloc_link_buffer(void **p, size_t bytes) {
+    return hipExtMallocWithFlags(p, bytes, hipDeviceMallocFinegrained);
+}
+
 int nw_colband_layout(int64_t n1, int64_t n2, int32_t nbands, int32_t r, const nw_params *p,
                       int64_t *strip_first, int64_t *strip_count, int64_t *start, int64_t *n_cols) {
     int64_t sf = 0, sc = 0, st = 0, nc = 0;
@@ -482,7 +491,7 @@ int nw_feed_alloc(int device, int64_t n2, uint64_t **d_feed) {
     if (device >= 0) NW_HIP_TRY(hipSetDevice(device));
     void *q = nullptr;
     const size_t bytes = (size_t)nw_feed_bytes(n2);
-    hipError_t e = hipMalloc(&q, bytes);
+    hipError_t e = alloc_link_buffer(&q, bytes);
     if (e != hipSuccess) return e == hipErrorOutOfMemory ? NW_ERR_OOM : NW_ERR_HIP;
     if (hipMemset(q, 0, bytes) != hipSuccess) {
         (void)hipFree(q);
@@ -500,7 +509,7 @@ int nw_halo_alloc(int device, int64_t n1, uint64_t **d_halo) {
     if (device >= 0) NW_HIP_TRY(hipSetDevice(device));
     void *p = nullptr;
     const size_t bytes = (size_t)nw_halo_bytes(n1);
-    hipError_t e = hipMalloc(&p, bytes);  // its own allocation: exportable by IPC as is
+    hipError_t e = alloc_link_buffer(&p, bytes);
     if (e != hipSuccess) return e == hipErrorOutOfMemory ? NW_ERR_OOM : NW_ERR_HIP;
     if (hipMemset(p, 0, bytes) != hipSuccess) {
         (void)hipFree(p);
