@@ -1201,7 +1201,11 @@ __device__ __forceinline__ void store_strip_grp(const FillArgs &A, char *__restr
         trw[17] = 0;
         trw[18] = ts;
     }
-    // Row band: hand this ring's 64 columns of the last row to the next band (see store_strip)
+    // Row band: hand this ring's 64 columns of the last row to the next band (see
+    // store_strip) -- from the store wave that stored the row's right half, the
+    // later one; with the default kSPR = 1 for C = 1 that wave also stored the
+    // left half (the NW_SPR tuning override with NS > 1 is for timing builds)
+    static_assert(NS == 1 || L::kSPR != 1, "");
     if (A.halo_out != nullptr && ((nrows - 1 + kLagH) / BATCH) % NS == q && ctrl_load(A.ctrl + 1) == 0u) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");

@@ -104,9 +104,10 @@ class LocalBands:
 
 # Per-row pace (ns) of a strip in a store-saturated sweep, per strip shape (C, NC):
 # tools/rect_time.py on 65536 x 524288 (one pass of 256 strips): T = pace *
-# (n2 + 255 * 64 * NC) gives (4,1) 35.2 ms -> 65, (2,2) 33.1 -> 59.4, (1,4) 30.0 -> 50.9.
-# The three shapes share the strip width W = 256 columns.
-COLBAND_PACE_NS = {(4, 1): 65.0, (2, 2): 59.4, (1, 4): 50.9}
+# (n2 + 255 * 64 * NC) gives (4,1) 35.7 ms -> 66.1, (2,2) 37.0 -> 66.4, (1,4) 29.7 -> 50.3
+# (gpurun_out/rect_cb2.log, this round's final kernel).  The three shapes share the
+# strip width W = 256 columns.
+COLBAND_PACE_NS = {(4, 1): 66.1, (2, 2): 66.4, (1, 4): 50.3}
 
 
 def colband_model_ms(n1: int, n2: int, shape) -> float:
