@@ -252,3 +252,18 @@ def test_two_process_colbands_shared_gpu(torch_gpu):
     n1 = 2 * width
     want = oracle.score(nwhip.synth(1, n1), nwhip.synth(2, n2))
     assert res["score"] == want and res["n_gpus"] == 2 and res["config"]["n1"] == n1
+
+
+# ------------------------------------------------------------------ shape model (CPU)
+def test_colband_shape_model():
+    """The modelled critical path picks the fast-pace shape for a short strip chain and the
+    short-hop shape for a long one (DESIGN.md 'Multi-GPU'); an explicit shape is kept."""
+    n2 = 524288
+    assert nw_bands.colband_shape(65536, n2) == (1, 4)
+    assert nw_bands.colband_shape(8 * 65536, n2) == (4, 1)
+    assert nw_bands.colband_shape(8 * 65536, n2, 2, 2) == (2, 2)
+    for shape in nw_bands.COLBAND_PACE_NS:
+        c, nc = shape
+        assert 64 * c * nc == 256  # one strip width: every band boundary is a strip boundary
+        # monotone in the table width (more strips -> longer chain)
+        assert nw_bands.colband_model_ms(65536, n2, shape) < nw_bands.colband_model_ms(131072, n2, shape)
