@@ -418,9 +418,9 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
     c->last_col0 = (int)col0;
     if (sw) {
         // best cell: max over the strips, then the first row-major cell holding it
-        if (!c->swinfo) NW_HIP_TRY(hipMalloc(&c->swinfo, 16 * sizeof(int64_t)));
+        if (!c->swinfo) NW_HIP_TRY(hipMalloc(&c->swinfo, 16 * sizeof(int64_t)));  // [0..9] traceback info, [12] locate key
         int32_t *best = c->smax + s.nstrips;
-        uint64_t *key = (uint64_t *)(c->swinfo + 8);
+        uint64_t *key = (uint64_t *)(c->swinfo + 12);
         if (nw::launch_sw_locate(d_t, pitch, n1, n2, col0, (int32_t)(nw::kWave * s.K * s.NC), c->smax,
                                  (int32_t)s.nstrips, key, best, stream) != hipSuccess)
             return NW_ERR_HIP;
@@ -583,7 +583,7 @@ int nw_fill_device(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *d_s2
         // best cell (nw_sw.hip locate): score and its first row-major position
         uint64_t key = 0;
         NW_HIP_TRY(hipMemcpy(&score, c->smax + c->last_strips, 4, hipMemcpyDeviceToHost));
-        NW_HIP_TRY(hipMemcpy(&key, c->swinfo + 8, 8, hipMemcpyDeviceToHost));
+        NW_HIP_TRY(hipMemcpy(&key, c->swinfo + 12, 8, hipMemcpyDeviceToHost));
         out->end_i = score > 0 ? (int64_t)(key >> 32) : 0;
         out->end_j = score > 0 ? (int64_t)(key & 0xFFFFFFFFull) : 0;
     } else {
@@ -606,17 +606,20 @@ int nw_sw_traceback(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *d_s
     int st;
     const size_t need = (size_t)std::max<int64_t>(end_i + end_j + 1, 1);
     if ((st = grow((void **)&c->ops, &c->ops_cap, need)) != NW_OK) return st;
-    if (!c->swinfo) NW_HIP_TRY(hipMalloc(&c->swinfo, 16 * sizeof(int64_t)));
+    if (!c->swinfo) NW_HIP_TRY(hipMalloc(&c->swinfo, 16 * sizeof(int64_t)));  // [0..9] traceback info, [12] locate key
     NW_HIP_TRY(hipEventRecord(c->ev0, nullptr));
     if (nw::launch_sw_traceback(d_t, pitch, (const uint8_t *)d_s1, (const uint8_t *)d_s2, p->match, p->mismatch,
                                 p->gap, end_i, end_j, c->ops, (int64_t)need, c->swinfo, nullptr) != hipSuccess)
         return NW_ERR_HIP;
     NW_HIP_TRY(hipEventRecord(c->ev1, nullptr));
-    int64_t info[8];
+    int64_t info[10];
     NW_HIP_TRY(hipMemcpy(info, c->swinfo, sizeof info, hipMemcpyDeviceToHost));
     if (std::getenv("NW_TB_DEBUG"))  // traceback phase timers (s_memrealtime ticks)
-        std::fprintf(stderr, "nw_sw_traceback: windows %lld, load %.3f ms, classify %.3f ms, walk %.3f ms\n",
-                     (long long)info[7], info[4] * 1e-5, info[5] * 1e-5, info[6] * 1e-5);
+        std::fprintf(stderr,
+                     "nw_sw_traceback: windows %lld, load %.3f ms, classify %.3f ms (1-step %.3f, 2-step %.3f), "
+                     "walk %.3f ms\n",
+                     (long long)info[7], info[4] * 1e-5, info[5] * 1e-5, info[8] * 1e-5, info[9] * 1e-5,
+                     info[6] * 1e-5);
     float ms = 0.f;
     NW_HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
     std::memset(out, 0, sizeof *out);

@@ -114,6 +114,7 @@ __global__ __launch_bounds__(kTbThreads) void nw_sw_traceback(
     }
     __syncthreads();
     uint64_t tl = 0, tc = 0, tw = 0, nwin = 0;  // (thread 0) ticks loading / classifying / walking
+    uint64_t tc1 = 0, tc2 = 0;                  // (of tc: the 1-step codes, the 2-step codes)
     for (;;) {
         const int64_t i = st[0], j = st[1];
         if (i <= 0 || j <= 0 || st[3] != 0) break;
@@ -160,6 +161,7 @@ __global__ __launch_bounds__(kTbThreads) void nw_sw_traceback(
             code[e] = cd;
         }
         __syncthreads();
+        const uint64_t t1b = __builtin_amdgcn_s_memrealtime();
         // Multi-step codes by doubling, so that the walk below takes 4 moves per
         // dependent LDS read: a k-step code holds the moves from a cell (2 bits
         // each: 0 diag, 1 up, 2 left), their count and their total index step.
@@ -170,29 +172,27 @@ __global__ __launch_bounds__(kTbThreads) void nw_sw_traceback(
         #pragma unroll
         for (int kk = 0; kk < kTbPer; ++kk) {
             const int e = tid + kk * kTbThreads;
+            // branch-free (the loads of all 16 cells issue together): a non-move
+            // reads its own code again
             const uint8_t a = code[e];
-            uint32_t w = 0;
-            if (is_mv(a)) {
-                const uint8_t b = code[e - a];
-                w = is_mv(b) ? (mv1(a) | (mv1(b) << 2) | (2u << 4) | ((uint32_t)(a + b) << 6))
-                             : (mv1(a) | (1u << 4) | ((uint32_t)a << 6));
-            }
-            cc2[e] = (uint16_t)w;
+            const bool ma = is_mv(a);
+            const uint8_t b = code[e - (ma ? a : 0)];
+            const bool mb = ma && is_mv(b);
+            const uint32_t one = mv1(a) | (1u << 4) | ((uint32_t)a << 6);
+            const uint32_t two = mv1(a) | (mv1(b) << 2) | (2u << 4) | ((uint32_t)(a + b) << 6);
+            cc2[e] = (uint16_t)(mb ? two : ma ? one : 0u);
         }
         __syncthreads();
+        const uint64_t t1c = __builtin_amdgcn_s_memrealtime();
         uint32_t *c4 = (uint32_t *)win;
         #pragma unroll
         for (int kk = 0; kk < kTbPer; ++kk) {
             const int e = tid + kk * kTbThreads;
             const uint32_t a = cc2[e];
             const uint32_t na = (a >> 4) & 3u, da = a >> 6;
-            uint32_t w = (a & 15u) | (na << 8) | (da << 16);
-            if (na == 2) {
-                const uint32_t b = cc2[e - (int)da];
-                const uint32_t nb = (b >> 4) & 3u, db = b >> 6;
-                w = (a & 15u) | ((b & 15u) << 4) | ((na + nb) << 8) | ((da + db) << 16);
-            }
-            c4[e] = w;
+            const uint32_t b = cc2[e - (na == 2 ? (int)da : 0)];  // (branch-free, as above)
+            const uint32_t nb = na == 2 ? (b >> 4) & 3u : 0u, db = na == 2 ? b >> 6 : 0u;
+            c4[e] = (a & 15u) | ((na == 2 ? b & 15u : 0u) << 4) | ((na + nb) << 8) | ((da + db) << 16);
         }
         __syncthreads();
         const uint64_t t2 = __builtin_amdgcn_s_memrealtime();
@@ -238,6 +238,8 @@ __global__ __launch_bounds__(kTbThreads) void nw_sw_traceback(
         const uint64_t t3 = __builtin_amdgcn_s_memrealtime();
         tl += t1 - t0;
         tc += t2 - t1;
+        tc1 += t1b - t1;
+        tc2 += t1c - t1b;
         tw += t3 - t2;
         if (st[0] < 0) break;
     }
@@ -251,6 +253,8 @@ __global__ __launch_bounds__(kTbThreads) void nw_sw_traceback(
         info[5] = (int64_t)tc;
         info[6] = (int64_t)tw;
         info[7] = (int64_t)nwin;
+        info[8] = (int64_t)tc1;
+        info[9] = (int64_t)tc2;
     }
 }
 
