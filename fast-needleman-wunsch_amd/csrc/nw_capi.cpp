@@ -105,9 +105,15 @@ void tuned_shape(int64_t n1, int64_t n2, int32_t *c, int32_t *nc) {
 
 // col0: first swept column (1 when the table's column 1 starts a 256-byte line)
 Shape make_shape(int64_t n1, int64_t n2, int32_t waves_req, int32_t sub_req, int32_t nc_req,
-                 int cus, int64_t col0) {
+                 int cus, int64_t col0, bool sw = false) {
     Shape s;
-    if (sub_req <= 0 && nc_req <= 0) {
+    if (sub_req <= 0 && nc_req <= 0 && sw) {
+        // Smith-Waterman cells cost 4 VALU instead of 2, which moves the balance
+        // toward more compute waves: 65536^2 (tools/sw_shapes.py) (2,2) 7.15 ms,
+        // (4,1) 7.57, (2,1) 7.95, (1,4) 8.64
+        s.K = 2;
+        s.NC = 2;
+    } else if (sub_req <= 0 && nc_req <= 0) {
         tuned_shape(n1, n2, &s.K, &s.NC);
     } else {
         s.K = sub_req > 0 ? sub_req : 2;
@@ -316,7 +322,7 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
         if (band->halo_out && (p->flags & 1)) return NW_ERR_ARG;  // needs the real last row
     }
     NW_HIP_TRY(hipSetDevice(c->device));
-    Shape s = make_shape(n1, n2, p->waves, p->substrips, p->strip_waves, c->cus, col0);
+    Shape s = make_shape(n1, n2, p->waves, p->substrips, p->strip_waves, c->cus, col0, sw);
     if (!nw::shape_ok(s.K, s.NC)) return NW_ERR_ARG;
     if (cb) {  // this launch sweeps its band's strips only
         s.nstrips = strip_count;

@@ -174,11 +174,16 @@ static_assert(Lay<1, 4>::kBytes <= 160 * 1024, "ring must fit a CU's LDS");
 
 // Granules are system-scope: the same loads and stores serve a column band's
 // feed, which lives in the neighbouring GPU's HBM (written over xGMI).
+#ifdef NW_EXP_GRAN_AGENT  // timing experiment: agent-scope granules (no peer feeds)
+#define NW_GRAN_SCOPE __HIP_MEMORY_SCOPE_AGENT
+#else
+#define NW_GRAN_SCOPE __HIP_MEMORY_SCOPE_SYSTEM
+#endif
 __device__ __forceinline__ uint64_t gran_load(const uint64_t *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, NW_GRAN_SCOPE);
 }
 __device__ __forceinline__ void gran_store(uint64_t *p, uint64_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, NW_GRAN_SCOPE);
 }
 __device__ __forceinline__ uint32_t ctrl_load(const uint32_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
