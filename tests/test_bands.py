@@ -10,6 +10,7 @@ in-kernel halo hand-off -- bit-exact against the oracle's bands; and the
 multi-process bench path (2 ranks sharing the one GPU: IPC halo buffers, gloo
 control plane) checked against the oracle's score.
 """
+import datetime
 import json
 import os
 import socket
@@ -58,7 +59,8 @@ def _rank_main(rank, world, port, n1, n2, scheme, outdir):
     import torch
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=60))  # fail, never hang
     s1, s2 = oracle.synth(11, n1), oracle.synth(12, n2)
     rows, start = nwhip.band_layout(n2, world, rank)
     halo = None
@@ -76,6 +78,7 @@ def _rank_main(rank, world, port, n1, n2, scheme, outdir):
 
 
 @pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.timeout(240)
 def test_gloo_bands_reassemble_the_table(tmp_path, world):
     import torch.multiprocessing as mp
     n1, n2, scheme = 301, 257, (1, -1, -1)

@@ -12,6 +12,7 @@ fed through the in-kernel feed hand-off -- bit-exact against the oracle, repeate
 launches, refusals, and the multi-process bench path (--partition cols, 2 ranks
 sharing the GPU) against the oracle's score.
 """
+import datetime
 import json
 import os
 import socket
@@ -92,7 +93,8 @@ def _rank_main(rank, world, port, n1, n2, scheme, layout, outdir):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=60))  # fail, never hang
     s1, s2 = oracle.synth(21, n1), oracle.synth(22, n2)
     if layout == "reference":
         nc, st = oracle.colband_layout(n1, world, rank)
@@ -114,6 +116,7 @@ def _rank_main(rank, world, port, n1, n2, scheme, layout, outdir):
 
 @pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.parametrize("layout", ["reference", "strips"])
+@pytest.mark.timeout(240)
 def test_gloo_colbands_reassemble_the_table(tmp_path, world, layout):
     import torch.multiprocessing as mp
     n1, n2, scheme = 64 * 7 + 3, 211, (1, -1, -1)
