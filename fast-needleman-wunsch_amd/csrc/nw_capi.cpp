@@ -614,7 +614,7 @@ int nw_sw_traceback(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *d_s
     if ((st = grow((void **)&c->ops, &c->ops_cap, need)) != NW_OK) return st;
     if (!c->swinfo) NW_HIP_TRY(hipMalloc(&c->swinfo, 16 * sizeof(int64_t)));  // [0..9] traceback info, [12] locate key
     NW_HIP_TRY(hipEventRecord(c->ev0, nullptr));
-    if (nw::launch_sw_traceback(d_t, pitch, (const uint8_t *)d_s1, (const uint8_t *)d_s2, p->match, p->mismatch,
+    if (nw::launch_sw_traceback(d_t, pitch, n1, (const uint8_t *)d_s1, (const uint8_t *)d_s2, p->match, p->mismatch,
                                 p->gap, end_i, end_j, c->ops, (int64_t)need, c->swinfo, nullptr) != hipSuccess)
         return NW_ERR_HIP;
     NW_HIP_TRY(hipEventRecord(c->ev1, nullptr));

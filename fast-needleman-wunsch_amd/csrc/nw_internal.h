@@ -81,7 +81,7 @@ int launch_sw_locate(const int32_t *table, int64_t pitch, int64_t n1, int64_t n2
 // traceback from (end_i, end_j) (see nw_fill.hip nw_sw_traceback); ops[] gets one
 // byte per step from the end cell back (0 diag, 1 up, 2 left), info8[0] = steps,
 // [1] = begin row, [2] = begin column, [3] = status (0 ok, 1 ops buffer too small)
-int launch_sw_traceback(const int32_t *table, int64_t pitch, const uint8_t *s1, const uint8_t *s2,
+int launch_sw_traceback(const int32_t *table, int64_t pitch, int64_t n1, const uint8_t *s1, const uint8_t *s2,
                         int32_t match, int32_t mismatch, int32_t gap, int64_t end_i, int64_t end_j,
                         uint8_t *ops, int64_t ops_cap, int64_t *info, void *stream);
 

@@ -78,31 +78,40 @@ int launch_sw_locate(const int32_t *table, int64_t pitch, int64_t n1, int64_t n2
 }
 
 // Traceback: one workgroup of 1024 threads.  The table around the current cell
-// is staged in LDS a window at a time -- rows [i0, i] x columns [j0, j], at most
-// (kWin+1)^2 int32, every thread issuing all its loads before it waits -- with
-// the window's characters; all threads then classify every cell of the window
-// with the move the walk takes there, stored as the LDS index step of that move
-// (diag: W+1, if t == t[i-1][j-1] + s; else up: W, if t == t[i-1][j] + GAP; else
-// left: 1), or a stop code: t == 0 (or row / column 0 of the table), the window's
-// own top row / left column (the walk continues in the next window), or "no
-// move matches" (not a Smith-Waterman table).  Thread 0 then follows the codes --
-// per step one dependent LDS byte read, its op byte into an LDS buffer -- and all
+// (i, j) is staged in LDS a window at a time: a band of kBandW = 2B+1 cells around
+// the anti-diagonal-free "entry diagonal" through (i, j), over up to kBandR rows --
+// window cell (r, x) is table cell (i0 + r, j - (rows-1-r) + x - B).  A diagonal
+// move keeps x, up moves to x + 1, left to x - 1, so the three moves are the LDS
+// index steps W, W - 1 and 1.  Smith-Waterman paths are mostly diagonal, so a band
+// covers ~kBandR moves per window where a square window of the same LDS covers ~W.
+// Every thread issues all its loads before it waits; all threads then classify
+// every cell of the window with the move the walk takes there, stored as its
+// index step (diag if t == t[i-1][j-1] + s; else up if t == t[i-1][j] + GAP; else
+// left if t == t[i][j-1] + GAP), or a stop code: t == 0 (or row / column 0 of the
+// table), the window's top row or band side (the walk continues in the next
+// window from there), or "no move matches" (not a Smith-Waterman table).
+// Doubling passes turn the codes into 4-move codes and thread 0 follows them --
+// per 4 moves one dependent LDS read, the ops into an LDS buffer -- and all
 // threads copy the window's ops out together.
-constexpr int kWin = 127;                       // (kWin+1)^2 int32 = 64 KB of LDS
+constexpr int kBandB = 32;
+constexpr int kBandW = 2 * kBandB + 1;          // 65 cells per window row
+constexpr int kBandR = 252;                     // rows per window: 252 * 65 <= 16384 cells
 constexpr int kTbThreads = 1024;
-constexpr int kTbPer = ((kWin + 1) * (kWin + 1) + kTbThreads - 1) / kTbThreads;  // loads per thread
-constexpr uint8_t kMvLeft = 1, kMvUp = kWin + 1, kMvDiag = kWin + 2;  // index steps (W = kWin + 1)
+constexpr int kTbCells = kBandR * kBandW;
+constexpr int kTbPer = (kTbCells + kTbThreads - 1) / kTbThreads;  // cells per thread
+constexpr int kTbPad = kTbPer * kTbThreads;  // LDS arrays padded: no bounds checks (rows >= kBandR there)
+constexpr uint8_t kMvLeft = 1, kMvUp = kBandW - 1, kMvDiag = kBandW;  // index steps
 constexpr uint8_t kStop = 0, kEdge = 200, kBad = 255;
 __global__ __launch_bounds__(kTbThreads) void nw_sw_traceback(
-    const int32_t *__restrict__ table, int64_t pitch, const uint8_t *__restrict__ s1,
+    const int32_t *__restrict__ table, int64_t pitch, int64_t n1, const uint8_t *__restrict__ s1,
     const uint8_t *__restrict__ s2, int32_t match, int32_t mismatch, int32_t gap, int64_t end_i, int64_t end_j,
     uint8_t *__restrict__ ops, int64_t ops_cap, int64_t *__restrict__ info) {
-    constexpr int W = kWin + 1;
-    __shared__ int32_t win[W * W];
-    __shared__ uint8_t code[W * W];
-    __shared__ uint16_t cc2[W * W];
-    __shared__ uint16_t ob[W / 2 + 2];  // the window's moves, 4 per entry (2 bits each | count << 8)
-    __shared__ uint8_t c1[W], c2[W];
+    constexpr int W = kBandW, B = kBandB;
+    __shared__ int32_t win[kTbPad];
+    __shared__ uint8_t code[kTbPad];
+    __shared__ uint16_t cc2[kTbPad];
+    __shared__ uint16_t ob[kBandR / 2 + kBandW + 2];  // the window's moves, 4 per entry (2 bits each | count << 8)
+    __shared__ uint8_t c1[kBandR + kBandW], c2[kBandR];
     __shared__ int64_t st[5];  // i, j, steps, status (done flag in the sign of i), moves this window
     const int tid = threadIdx.x;
     if (tid == 0) {
@@ -120,42 +129,49 @@ __global__ __launch_bounds__(kTbThreads) void nw_sw_traceback(
         if (i <= 0 || j <= 0 || st[3] != 0) break;
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         ++nwin;
-        const int64_t i0 = i > kWin ? i - kWin : 0, j0 = j > kWin ? j - kWin : 0;
-        const int rows = (int)(i - i0 + 1), cols = (int)(j - j0 + 1);
+        const int rows = (int)(i + 1 < kBandR ? i + 1 : kBandR);
+        const int64_t i0 = i - (rows - 1);
+        const int64_t jb = j - (rows - 1) - B;  // table column of window cell (r, x) = jb + r + x
+        // r + x ranges over [0, kBandR + kBandW): the table's columns 1 and n1 as
+        // offsets from jb, clamped into that range (32-bit compares in the classify pass)
+        const int lo1 = (int)std::min<int64_t>(std::max<int64_t>(1 - jb, -1), kBandR + kBandW);
+        const int hi = (int)std::min<int64_t>(std::max<int64_t>(n1 - jb, -1), kBandR + kBandW);
         int32_t v[kTbPer];
 #pragma unroll
         for (int k = 0; k < kTbPer; ++k) {
-            const int e = tid + k * kTbThreads, r = e / W, c = e % W;
-            v[k] = (r < rows && c < cols) ? table[(i0 + r) * pitch + j0 + c] : 0;
+            const int e = tid + k * kTbThreads, r = e / W, x = e % W;
+            const int64_t gj = jb + r + x;
+            v[k] = (e < kTbCells && r < rows && gj >= 0 && gj <= n1) ? table[(i0 + r) * pitch + gj] : 0;
         }
 #pragma unroll
         for (int k = 0; k < kTbPer; ++k) {
             const int e = tid + k * kTbThreads;
-            if (e < W * W) win[e] = v[k];
+            if (e < kTbCells) win[e] = v[k];
         }
-        if (tid < W) {
-            c1[tid] = (tid >= 1 && tid < cols) ? s1[j0 + tid - 1] : 0;  // column j0 + c holds s1[j0 + c - 1]
-            c2[tid] = (tid >= 1 && tid < rows) ? s2[i0 + tid - 1] : 0;
+        if (tid < kBandR + kBandW) {  // c1[r + x] = s1 character of column jb + r + x
+            const int64_t gj = jb + tid;
+            c1[tid] = (gj >= 1 && gj <= n1) ? s1[gj - 1] : 0;
         }
+        if (tid < kBandR) c2[tid] = (tid < rows && i0 + tid >= 1) ? s2[i0 + tid - 1] : 0;
         __syncthreads();
         const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
         #pragma unroll
         for (int kk = 0; kk < kTbPer; ++kk) {
             const int e = tid + kk * kTbThreads;
-            const int r = e / W, c = e % W;
+            const int r = e / W, x = e - r * W, q = r + x;
             uint8_t cd = kStop;
-            if (r >= rows || c >= cols) {
-                cd = kStop;  // (never reached: the walk starts at the bottom-right cell)
-            } else if (r == 0 || c == 0) {
-                cd = (i0 + r == 0 || j0 + c == 0) ? kStop : kEdge;
+            if (r >= rows || q < lo1 || q > hi || i0 + r == 0) {
+                cd = kStop;  // (outside the table, or its row / column 0)
+            } else if (r == 0 || x == 0 || x == W - 1) {
+                cd = kEdge;  // a neighbour lies outside the window
             } else {
                 const int32_t t = win[e];
                 if (t > 0) {
-                    const int32_t sc = c1[c] == c2[r] ? match : mismatch;
-                    cd = t == win[e - W - 1] + sc ? kMvDiag
-                         : t == win[e - W] + gap  ? kMvUp
-                         : t == win[e - 1] + gap  ? kMvLeft
-                                                  : kBad;
+                    const int32_t sc = c1[q] == c2[r] ? match : mismatch;
+                    cd = t == win[e - W] + sc        ? kMvDiag
+                         : t == win[e - W + 1] + gap ? kMvUp
+                         : t == win[e - 1] + gap     ? kMvLeft
+                                                     : kBad;
                 }
             }
             code[e] = cd;
@@ -197,7 +213,7 @@ __global__ __launch_bounds__(kTbThreads) void nw_sw_traceback(
         __syncthreads();
         const uint64_t t2 = __builtin_amdgcn_s_memrealtime();
         if (tid == 0) {
-            int idx = (rows - 1) * W + (cols - 1);
+            int idx = (rows - 1) * W + B;
             int k = 0, q = 0;
             for (;;) {
                 const uint32_t w = c4[idx];
@@ -209,7 +225,7 @@ __global__ __launch_bounds__(kTbThreads) void nw_sw_traceback(
                 if (n < 4) break;
             }
             const uint8_t d = code[idx];  // where the walk stopped: kStop, kEdge or kBad
-            const int r = idx / W, c = idx % W;
+            const int r = idx / W, x = idx % W;
             const int64_t steps = st[2];
             if (d == kBad) {
                 st[3] = 2;  // not a Smith-Waterman table
@@ -217,7 +233,7 @@ __global__ __launch_bounds__(kTbThreads) void nw_sw_traceback(
                 st[3] = 1;
             } else {
                 st[0] = d == kStop ? -(i0 + r) - 1 : i0 + r;  // (kEdge: next window from here)
-                st[1] = j0 + c;
+                st[1] = jb + r + x;
             }
             st[4] = k;
         }
@@ -258,10 +274,10 @@ __global__ __launch_bounds__(kTbThreads) void nw_sw_traceback(
     }
 }
 
-int launch_sw_traceback(const int32_t *table, int64_t pitch, const uint8_t *s1, const uint8_t *s2,
+int launch_sw_traceback(const int32_t *table, int64_t pitch, int64_t n1, const uint8_t *s1, const uint8_t *s2,
                         int32_t match, int32_t mismatch, int32_t gap, int64_t end_i, int64_t end_j,
                         uint8_t *ops, int64_t ops_cap, int64_t *info, void *stream) {
-    hipLaunchKernelGGL(nw_sw_traceback, dim3(1), dim3(kTbThreads), 0, (hipStream_t)stream, table, pitch, s1, s2, match,
+    hipLaunchKernelGGL(nw_sw_traceback, dim3(1), dim3(kTbThreads), 0, (hipStream_t)stream, table, pitch, n1, s1, s2, match,
                        mismatch, gap, end_i, end_j, ops, ops_cap, info);
     return (int)hipGetLastError();
 }
