@@ -79,7 +79,7 @@ int launch_sw_locate(const int32_t *table, int64_t pitch, int64_t n1, int64_t n2
 
 // Traceback: one workgroup of 1024 threads.  The table around the current cell
 // (i, j) is staged in LDS a window at a time: a band of kBandW = 2B+1 cells around
-// the anti-diagonal-free "entry diagonal" through (i, j), over up to kBandR rows --
+// the diagonal through (i, j) (the "entry diagonal"), over up to kBandR rows --
 // window cell (r, x) is table cell (i0 + r, j - (rows-1-r) + x - B).  A diagonal
 // move keeps x, up moves to x + 1, left to x - 1, so the three moves are the LDS
 // index steps W, W - 1 and 1.  Smith-Waterman paths are mostly diagonal, so a band
