@@ -6,8 +6,11 @@ A "step" is one complete fill of the table (device-resident: sequences and
 table in HBM before the timed region; nothing copied back inside it).
 
   N = 1 : BASELINE config 3 -- 262144 x 262144 int32 table (275 GB) on one GPU.
-  N > 1 : row bands across ranks (mpi-horz contract), n1 = 524288 columns and
-          65536 rows per GPU (weak scaling; N = 8 is BASELINE config 4, 512k x 512k);
+  N > 1 : `value` = row bands across ranks (mpi-horz contract, BASELINE config 4):
+          n1 = 524288 columns and 65536 rows per GPU (weak scaling; N = 8 is
+          512k x 512k); column bands (mpi-vert: 65536 columns per GPU x 524288
+          rows) run after it as `alt_partition`.  Launches are enqueued back to
+          back (link-word flow control, no host round trip between them);
           fast-needleman-wunsch_amd/nw_bands.py, DESIGN.md "Multi-GPU".
 
 Prints ONE JSON line on rank 0 (see README / DESIGN.md for field meanings).
@@ -42,9 +45,13 @@ def parse():
     ap.add_argument("--band-rows", type=int, default=65536,
                     help="N>1: rows per GPU band (weak scaling; N=8 -> 512k x 512k, config 4)")
     ap.add_argument("--band-cols", type=int, default=524288, help="N>1: table columns n1")
-    ap.add_argument("--partition", choices=["rows", "cols"], default="cols",
-                    help="N>1: column bands (mpi-vert; default: the shorter critical path, "
-                         "DESIGN.md 'Multi-GPU') or row bands (mpi-horz, config 4's partition)")
+    ap.add_argument("--partition", choices=["rows", "cols"], default="rows",
+                    help="N>1: the partition reported as `value`: row bands (mpi-horz, BASELINE "
+                         "config 4; default) or column bands (mpi-vert)")
+    ap.add_argument("--alt-partition", choices=["rows", "cols", "none"], default=None,
+                    help="N>1: the partition reported as `alt_partition` (default: the other one)")
+    ap.add_argument("--kernel", type=int, default=0,
+                    help="0 auto, 1 anti-diagonal strips, 2 row-scan panels (nw_params.kernel)")
     ap.add_argument("--col-width", type=int, default=65536,
                     help="N>1 column bands: columns per GPU (weak scaling; n1 = N x this)")
     ap.add_argument("--col-rows", type=int, default=524288, help="N>1 column bands: table rows n2")
@@ -281,8 +288,9 @@ def main():
         return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus > 1 or world > 1:
-        from nw_bands import run_bands  # multi-GPU row bands
-        run_bands(args)
+        import nw_bands  # multi-GPU row bands (+ column bands as the alternate leg)
+        nw_bands.cpu_baseline_fn = cpu_baseline
+        nw_bands.run_bands(args)
         return
     run_single(args)
 

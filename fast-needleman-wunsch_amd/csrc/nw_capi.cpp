@@ -42,6 +42,7 @@ struct nw_ctx {
     size_t ops_cap = 0;
     int64_t *swinfo = nullptr;  // SW traceback info (4 words) + locate key
     int last_col0 = 0;
+    int last_kernel = NW_KERNEL_STRIPS;
 };
 
 namespace {
@@ -76,6 +77,7 @@ struct Shape {
     int64_t nRows, nCols, nstrips, nblocks, waves, M, gstride;
     int64_t waves_max;  // resident strip workgroups (before capping at nstrips)
     int32_t K, NC;
+    int32_t kernel;     // NW_KERNEL_STRIPS or NW_KERNEL_PANELS
 };
 
 constexpr int kLdsPerCU = 160 * 1024;
@@ -104,10 +106,35 @@ void tuned_shape(int64_t n1, int64_t n2, int32_t *c, int32_t *nc) {
 }
 
 // col0: first swept column (1 when the table's column 1 starts a 256-byte line)
+// Panel shape for nw_params.kernel = PANELS with substrips = strip_waves = 0:
+// the widest panel that still gives every CU a panel (a panel is one CU's
+// work; the 256k square has 262144 / 1024 = 256 of (4,4)).
+void panel_auto(int64_t n1, int cus, int32_t *c, int32_t *nw) {
+    const int64_t cols = n1 + 1;
+    if (cols >= (int64_t)cus * 1024) {
+        *c = 4;
+        *nw = 4;
+    } else if (cols >= (int64_t)cus * 512) {
+        *c = 2;
+        *nw = 4;
+    } else {
+        *c = 4;
+        *nw = 1;
+    }
+}
+
 Shape make_shape(int64_t n1, int64_t n2, int32_t waves_req, int32_t sub_req, int32_t nc_req,
-                 int cus, int64_t col0, bool sw = false) {
+                 int cus, int64_t col0, bool sw = false, int32_t kernel_req = NW_KERNEL_AUTO) {
     Shape s;
-    if (sub_req <= 0 && nc_req <= 0 && sw) {
+    s.kernel = kernel_req == NW_KERNEL_PANELS ? NW_KERNEL_PANELS : NW_KERNEL_STRIPS;
+    if (s.kernel == NW_KERNEL_PANELS) {
+        if (sub_req <= 0 && nc_req <= 0) {
+            panel_auto(n1, cus, &s.K, &s.NC);
+        } else {
+            s.K = sub_req > 0 ? sub_req : 4;
+            s.NC = nc_req > 0 ? nc_req : (s.K == 4 ? 4 : s.K == 2 ? 8 : 8);
+        }
+    } else if (sub_req <= 0 && nc_req <= 0 && sw) {
         // Smith-Waterman cells cost 4 VALU instead of 2, which moves the balance
         // toward more compute waves: 65536^2 (tools/sw_shapes.py) (2,2) 7.15 ms,
         // (4,1) 7.57, (2,1) 7.95, (1,4) 8.64
@@ -124,8 +151,11 @@ Shape make_shape(int64_t n1, int64_t n2, int32_t waves_req, int32_t sub_req, int
     const int64_t width = (int64_t)nw::kWave * s.K * s.NC;
     s.nstrips = std::max<int64_t>(1, (s.nCols - col0 + width - 1) / width);
     s.nblocks = (s.nRows + nw::kWave - 1) / nw::kWave;
-    // one strip workgroup per LDS ring set; as many as fit in a CU's LDS
-    const int64_t per_cu = std::max(1, kLdsPerCU / nw::lds_bytes(s.K, s.NC));
+    // one strip workgroup per LDS ring set; as many as fit in a CU's LDS (a
+    // panel workgroup is 2 * NW waves: at most 32 waves per CU)
+    const int lds = s.kernel == NW_KERNEL_PANELS ? nw::panel_lds_bytes(s.K, s.NC) : nw::lds_bytes(s.K, s.NC);
+    int64_t per_cu = std::max(1, kLdsPerCU / std::max(lds, 1));
+    if (s.kernel == NW_KERNEL_PANELS) per_cu = std::min<int64_t>(per_cu, std::max(1, 32 / (2 * s.NC)));
     int64_t w = waves_req > 0 ? waves_req : per_cu * cus;
     s.waves_max = std::max<int64_t>(1, w);
     s.waves = std::max<int64_t>(1, std::min<int64_t>(w, s.nstrips));
@@ -138,13 +168,19 @@ Shape make_shape(int64_t n1, int64_t n2, int32_t waves_req, int32_t sub_req, int
 
 bool fits_i8(int32_t x) { return x >= -128 && x <= 127; }
 
+bool shape_valid(const Shape &s) {
+    return s.kernel == NW_KERNEL_PANELS ? nw::panel_shape_ok(s.K, s.NC) : nw::shape_ok(s.K, s.NC);
+}
+
 bool valid_params(const nw_params *p) {
     if (!p) return false;
     if (p->mode != NW_MODE_NW && p->mode != NW_MODE_SW) return false;
     if (p->mode == NW_MODE_SW && p->gap > 0) return false;  // local alignment needs a penalty
     if (p->substrips != 0 && p->substrips != 1 && p->substrips != 2 && p->substrips != 4) return false;
-    if (p->strip_waves != 0 && p->strip_waves != 1 && p->strip_waves != 2 && p->strip_waves != 4)
+    if (p->strip_waves != 0 && p->strip_waves != 1 && p->strip_waves != 2 && p->strip_waves != 4 &&
+        p->strip_waves != 8)
         return false;
+    if (p->kernel != NW_KERNEL_AUTO && p->kernel != NW_KERNEL_STRIPS && p->kernel != NW_KERNEL_PANELS) return false;
     if (p->timeout_ms < 0) return false;
     // keep every intermediate far from int32 overflow (|score| < 2^29)
     const int32_t lim = 1 << 12;
@@ -199,6 +235,11 @@ int64_t nw_table_offset(void) { return nw::kWave - 1; }
 int64_t nw_strip_lds_bytes(int32_t substrips, int32_t strip_waves) {
     if (!nw::shape_ok(substrips, strip_waves)) return -1;
     return nw::lds_bytes(substrips, strip_waves);
+}
+
+int64_t nw_panel_lds_bytes(int32_t substrips, int32_t strip_waves) {
+    if (!nw::panel_shape_ok(substrips, strip_waves)) return -1;
+    return nw::panel_lds_bytes(substrips, strip_waves);
 }
 
 int64_t nw_ctx_workspace_bytes(int64_t n1, int64_t n2, int32_t waves) {
@@ -256,8 +297,8 @@ void nw_ctx_destroy(nw_ctx *c) {
 static int colband_layout(int64_t n1, int64_t n2, int32_t nb, int32_t r, const nw_params *p, int cus,
                    int64_t *sf, int64_t *sc, int64_t *start, int64_t *ncols) {
     if (!p || n1 < 1 || n2 < 0 || nb < 1 || r < 0 || r >= nb) return NW_ERR_ARG;
-    const Shape s = make_shape(n1, n2, 0, p->substrips, p->strip_waves, cus, 1);
-    if (!nw::shape_ok(s.K, s.NC) || nb > s.nstrips) return NW_ERR_ARG;
+    const Shape s = make_shape(n1, n2, 0, p->substrips, p->strip_waves, cus, 1, false, p->kernel);
+    if (!shape_valid(s) || nb > s.nstrips) return NW_ERR_ARG;
     const int64_t W = (int64_t)nw::kWave * s.K * s.NC;
     const int64_t base = s.nstrips / nb, extra = s.nstrips % nb;
     *sf = r * base + std::min<int64_t>(r, extra);
@@ -322,14 +363,15 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
         if (band->halo_out && (p->flags & 1)) return NW_ERR_ARG;  // needs the real last row
     }
     NW_HIP_TRY(hipSetDevice(c->device));
-    Shape s = make_shape(n1, n2, p->waves, p->substrips, p->strip_waves, c->cus, col0, sw);
-    if (!nw::shape_ok(s.K, s.NC)) return NW_ERR_ARG;
+    Shape s = make_shape(n1, n2, p->waves, p->substrips, p->strip_waves, c->cus, col0, sw, p->kernel);
+    if (!shape_valid(s)) return NW_ERR_ARG;
+    const bool panels = s.kernel == NW_KERNEL_PANELS;
     if (cb) {  // this launch sweeps its band's strips only
         s.nstrips = strip_count;
         s.waves = std::max<int64_t>(1, std::min<int64_t>(s.waves_max, s.nstrips));
         s.M = std::min<int64_t>(s.nstrips, s.waves + 1);
     }
-    if (sw && !nw::sw_shape_ok(s.K, s.NC)) return NW_ERR_UNSUPPORTED;
+    if (sw && !panels && !nw::sw_shape_ok(s.K, s.NC)) return NW_ERR_UNSUPPORTED;
     if (s.nstrips > INT32_MAX / 2 || s.nblocks > INT32_MAX / 2) return NW_ERR_ARG;
 
     int st;
@@ -345,7 +387,8 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
         NW_HIP_TRY(hipMemsetAsync(c->gran, 0, c->gran_cap, (hipStream_t)stream));
         c->tagbase = 1;
     }
-    if ((uint64_t)c->tagbase + (uint64_t)s.nstrips + 2u >= 0xFFFFFFF0ull) {
+    // tags run up to tagbase + strip0 + nstrips (p is the GLOBAL strip index)
+    if ((uint64_t)c->tagbase + (uint64_t)strip_first + (uint64_t)s.nstrips + 2u >= 0xFFFFFFF0ull) {
         NW_HIP_TRY(hipMemsetAsync(c->gran, 0, c->gran_cap, (hipStream_t)stream));
         c->tagbase = 1;
     }
@@ -360,8 +403,10 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
     // v_perm score tables when every substitution score minus 2*GAP fits int8
     // (the kernel falls back to compares on the device when s1 holds more than
     // kMaxPerm distinct characters).
-    const int32_t gw = sw ? 0 : p->gap;  // the w form's offset (NW only)
-    const bool perm_ok = fits_i8(p->match - 2 * gw) && fits_i8(p->mismatch - 2 * gw) &&
+    // table bytes are s - 2 GAP in the w form (NW), s (strips) / s - GAP (panels,
+    // the u form) for SW
+    const int32_t off = !sw ? 2 * p->gap : panels ? p->gap : 0;
+    const bool perm_ok = fits_i8(p->match - off) && fits_i8(p->mismatch - off) &&
                          !(p->flags & NW_FLAG_NO_PROFILE);
     if (sw) {
         // per-strip best cells (zeroed on the launch stream) + best / key words
@@ -411,17 +456,20 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
     a.timeout_ticks = (uint64_t)(p->timeout_ms > 0 ? p->timeout_ms : 20000) * 100000ull;
     a.sw = sw ? 1 : 0;
     a.smax = sw ? c->smax : nullptr;
-    if (nw::launch_fill(a, s.K, s.NC, (int)s.waves, stream) != hipSuccess) return NW_ERR_HIP;
+    if ((panels ? nw::launch_panels(a, s.K, s.NC, (int)s.waves, stream)
+                : nw::launch_fill(a, s.K, s.NC, (int)s.waves, stream)) != hipSuccess)
+        return NW_ERR_HIP;
     // a column band's local column 0 (band r-1's last column) from its feed
     if (cb && cb->feed_in &&
         nw::launch_colband_edge(cb->feed_in, d_t, pitch, n2, p->gap, start, stream) != hipSuccess)
         return NW_ERR_HIP;
-    c->tagbase += (uint32_t)s.nstrips + 1u;
+    c->tagbase += (uint32_t)(strip_first + s.nstrips) + 1u;
     c->last_waves = (int)s.waves;
     c->last_strips = (int)s.nstrips;
     c->last_sub = s.K;
     c->last_nc = s.NC;
     c->last_col0 = (int)col0;
+    c->last_kernel = s.kernel;
     if (sw) {
         // best cell: max over the strips, then the first row-major cell holding it
         if (!c->swinfo) NW_HIP_TRY(hipMalloc(&c->swinfo, 16 * sizeof(int64_t)));  // [0..9] traceback info, [12] locate key
@@ -531,6 +579,38 @@ int nw_halo_free(uint64_t *d_halo) {
     return NW_OK;
 }
 
+int nw_link_alloc(int device, uint32_t **d_word) {
+    if (!d_word) return NW_ERR_ARG;
+    *d_word = nullptr;
+    if (device >= 0) NW_HIP_TRY(hipSetDevice(device));
+    void *q = nullptr;
+    hipError_t e = alloc_link_buffer(&q, 256);
+    if (e != hipSuccess) return e == hipErrorOutOfMemory ? NW_ERR_OOM : NW_ERR_HIP;
+    if (hipMemset(q, 0, 256) != hipSuccess) {
+        (void)hipFree(q);
+        return NW_ERR_HIP;
+    }
+    *d_word = (uint32_t *)q;
+    return NW_OK;
+}
+
+int nw_link_wait_async(uint32_t *d_word, uint32_t value, int32_t timeout_ms, void *stream) {
+    if (!d_word || timeout_ms < 0) return NW_ERR_ARG;
+    const uint64_t ticks = (uint64_t)(timeout_ms > 0 ? timeout_ms : 20000) * 100000ull;
+    return nw::launch_link_wait(d_word, value, ticks, stream) == hipSuccess ? NW_OK : NW_ERR_HIP;
+}
+
+int nw_link_signal_async(uint32_t *d_word, uint32_t value, void *stream) {
+    if (!d_word) return NW_ERR_ARG;
+    return nw::launch_link_signal(d_word, value, stream) == hipSuccess ? NW_OK : NW_ERR_HIP;
+}
+
+int nw_link_status(const uint32_t *d_word, uint32_t *out) {
+    if (!d_word || !out) return NW_ERR_ARG;
+    NW_HIP_TRY(hipMemcpy(out, d_word + 1, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return NW_OK;
+}
+
 int nw_ipc_get_handle(const void *d_ptr, void *handle) {
     if (!d_ptr || !handle) return NW_ERR_ARG;
     hipIpcMemHandle_t h;
@@ -584,6 +664,7 @@ int nw_fill_device(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *d_s2
     out->waves = c->last_waves;
     out->substrips = c->last_sub;
     out->strip_waves = c->last_nc;
+    out->kernel = c->last_kernel;
     int32_t score = 0;
     if (p->mode == NW_MODE_SW) {
         // best cell (nw_sw.hip locate): score and its first row-major position

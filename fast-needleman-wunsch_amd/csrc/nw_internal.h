@@ -92,6 +92,14 @@ int launch_rowpack(const uint8_t *d_s1, int64_t n1, const uint8_t *d_s2, int64_t
 bool shape_ok(int substrips, int strip_waves);
 int launch_fill(const FillArgs &a, int substrips, int strip_waves, int grid, void *stream);
 int lds_bytes(int substrips, int strip_waves);
+// Row-scan panels (nw_rows.hip): shapes (C columns per lane, NW compute waves)
+bool panel_shape_ok(int c, int nwaves);
+int panel_lds_bytes(int c, int nwaves);
+int launch_panels(const FillArgs &a, int c, int nwaves, int grid, void *stream);
+// Band-to-band flow control (nw_link.hip): wait until word[0] >= value (word[1]
+// records a timeout), or store word[0] = value; one-lane kernels on `stream`
+int launch_link_wait(uint32_t *word, uint32_t value, uint64_t ticks, void *stream);
+int launch_link_signal(uint32_t *word, uint32_t value, void *stream);
 int64_t rowpack_len(int32_t nblocks);  // 16-byte entries
 const char *kernel_variant();
 

@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "nw_internal.h"
 
 namespace nw {
@@ -35,11 +37,14 @@ __global__ __launch_bounds__(256) void nw_sw_best(const int32_t *__restrict__ sm
     }
 }
 
-// First row-major cell holding the best value: workgroup (p, rb) scans strip p's
-// columns over rows [rb*kLocRows, ...) if the strip's maximum is the best one;
-// each thread keeps the first row of its column, the workgroup and then the grid
-// take the minimum key (row << 32 | column).
+// First row-major cell holding the best value: workgroup (p, y) scans strip /
+// panel p's columns (any width: 256 at a time) over the row blocks y, y +
+// gridDim.y, ... of kLocRows rows if the strip's maximum is the best one; each
+// thread keeps the first row of its column, the workgroup and then the grid take
+// the minimum key (row << 32 | column).  gridDim.y is capped (the y dimension of
+// a grid is limited), tall tables loop.
 constexpr int kLocRows = 512;
+constexpr int kLocMaxY = 4096;
 __global__ __launch_bounds__(256) void nw_sw_locate(const int32_t *__restrict__ table, int64_t pitch,
                                                     int64_t n1, int64_t n2, int64_t col0, int32_t strip_cols,
                                                     const int32_t *__restrict__ smax,
@@ -51,18 +56,25 @@ __global__ __launch_bounds__(256) void nw_sw_locate(const int32_t *__restrict__ 
     __shared__ unsigned long long kmin;
     if (threadIdx.x == 0) kmin = ~0ull;
     __syncthreads();
-    const int64_t c = col0 + (int64_t)p * strip_cols + threadIdx.x;
-    const int64_t r0 = (int64_t)blockIdx.y * kLocRows;
-    const int64_t r1 = min(r0 + kLocRows, n2 + 1);
-    if ((int)threadIdx.x < strip_cols && c <= n1) {
-        for (int64_t r = r0; r < r1; ++r) {
-            if (table[r * pitch + c] == b) {
-                atomicMin(&kmin, ((unsigned long long)r << 32) | (unsigned long long)c);
-                break;
+    const int64_t nblk = (n2 + kLocRows) / kLocRows;
+    for (int64_t y = blockIdx.y; y < nblk; y += gridDim.y) {
+        const int64_t r0 = y * kLocRows;
+        const int64_t r1 = min(r0 + kLocRows, n2 + 1);
+        for (int32_t x = threadIdx.x; x < strip_cols; x += 256) {
+            const int64_t c = col0 + (int64_t)p * strip_cols + x;
+            if (c > n1) break;
+            for (int64_t r = r0; r < r1; ++r) {
+                if (table[r * pitch + c] == b) {
+                    atomicMin(&kmin, ((unsigned long long)r << 32) | (unsigned long long)c);
+                    break;
+                }
             }
         }
+        // a later row block cannot hold an earlier row: stop once one matched
+        __syncthreads();
+        if (kmin != ~0ull) break;
+        __syncthreads();
     }
-    __syncthreads();
     if (threadIdx.x == 0 && kmin != ~0ull) atomicMin((unsigned long long *)key, kmin);
 }
 
@@ -71,7 +83,7 @@ int launch_sw_locate(const int32_t *table, int64_t pitch, int64_t n1, int64_t n2
                      void *stream) {
     hipStream_t s = (hipStream_t)stream;
     hipLaunchKernelGGL(nw_sw_best, dim3(1), dim3(256), 0, s, smax, nstrips, best, key);
-    const int64_t rb = (n2 + 1 + kLocRows - 1) / kLocRows;
+    const int64_t rb = std::min<int64_t>((n2 + kLocRows) / kLocRows, kLocMaxY);
     hipLaunchKernelGGL(nw_sw_locate, dim3((unsigned)nstrips, (unsigned)rb), dim3(256), 0, s, table, pitch, n1, n2,
                        col0, strip_cols, smax, best, key);
     return (int)hipGetLastError();

@@ -40,12 +40,34 @@ def plan(n2: int, nbands: int):
     return [nwhip.band_layout(n2, nbands, r) for r in range(nbands)]
 
 
-def resident_waves(device: int = 0, substrips: int = 0, strip_waves: int = 0) -> int:
-    """Persistent strip workgroups that fit on the device at once (LDS-bound:
-    nw_strip_lds_bytes per workgroup, 160 KiB per CU)."""
+def resident_waves(device: int = 0, substrips: int = 0, strip_waves: int = 0, kernel: int = 0) -> int:
+    """Persistent strip / panel workgroups that fit on the device at once
+    (LDS-bound: nw_strip_lds_bytes / nw_panel_lds_bytes per workgroup, 160 KiB per
+    CU; a panel workgroup of 2 * NW waves also counts against 32 waves per CU)."""
     import torch
     cus = torch.cuda.get_device_properties(device).multi_processor_count
+    if kernel == nwhip.KERNEL_PANELS:
+        c, nw = substrips or 4, strip_waves or 1
+        return cus * max(1, min(LDS_PER_CU // nwhip.panel_lds_bytes(c, nw), 32 // (2 * nw)))
     return cus * (LDS_PER_CU // nwhip.strip_lds_bytes(*nwhip.strip_shape(substrips, strip_waves)))
+
+
+def panel_shape_for(cols: int, cus: int = 256):
+    """Panel shape (C, NW) for a sweep of `cols` columns on `cus` CUs: the widest
+    panel that still gives every CU one (nw_capi.cpp panel_auto)."""
+    if cols >= cus * 1024:
+        return 4, 4
+    if cols >= cus * 512:
+        return 2, 4
+    return 4, 1
+
+
+def band_shape(n1: int, n2_band: int, substrips: int = 0, strip_waves: int = 0, kernel: int = 0):
+    """Shape of a row-band fill: the caller's, else strips: the tuned shape for
+    a band of this size; panels: panel_shape_for(n1)."""
+    if kernel == nwhip.KERNEL_PANELS:
+        return (substrips, strip_waves) if (substrips or strip_waves) else panel_shape_for(n1 + 1)
+    return nwhip.strip_shape(substrips, strip_waves, n1, n2_band)
 
 
 class LocalBands:
@@ -55,20 +77,20 @@ class LocalBands:
     co-resident (a band waiting for its halo never blocks its producer)."""
 
     def __init__(self, n1: int, n2: int, nbands: int, device: int = 0, substrips: int = 0,
-                 strip_waves: int = 0):
+                 strip_waves: int = 0, kernel: int = 0):
         import torch
-        self.n1, self.n2, self.P, self.device = n1, n2, nbands, device
+        self.n1, self.n2, self.P, self.device, self.kernel = n1, n2, nbands, device, kernel
         self.layout = plan(n2, nbands)
         # one shape for every band (auto: the tuned shape for a band of this size)
-        self.substrips, self.strip_waves = nwhip.strip_shape(
-            substrips, strip_waves, n1, max(rows for rows, _ in self.layout) - 1)
+        self.substrips, self.strip_waves = band_shape(
+            n1, max(rows for rows, _ in self.layout) - 1, substrips, strip_waves, kernel)
         if any(rows < 1 for rows, _ in self.layout):
             raise ValueError(f"{nbands} bands need at least {nbands} rows (n2+1 = {n2 + 1})")
         self.tables = [nwhip.Context.alloc_table(n1, rows - 1) for rows, _ in self.layout]
         self.halos = [None] + [nwhip.Halo(n1, device) for _ in range(nbands - 1)]
         self.ctxs = [nwhip.Context(device) for _ in range(nbands)]
         self.streams = [torch.cuda.Stream(device) for _ in range(nbands)]
-        self.waves = max(1, resident_waves(device, self.substrips, self.strip_waves) // nbands)
+        self.waves = max(1, resident_waves(device, self.substrips, self.strip_waves, kernel) // nbands)
         self.tag = 0
 
     def fill(self, d_s1, d_s2, scheme=(1, 0, -1), flags: int = 0, timeout_ms: int = 0) -> int:
@@ -85,7 +107,7 @@ class LocalBands:
                 halo_out=self.halos[r + 1].ptr if r + 1 < self.P else None,
                 tag=self.tag, scheme=scheme, waves=self.waves, stream=st, flags=flags,
                 substrips=self.substrips, strip_waves=self.strip_waves, row0=start,
-                timeout_ms=timeout_ms)
+                timeout_ms=timeout_ms, kernel=self.kernel)
         for r, st in enumerate(self.streams):
             s = self.ctxs[r].status(st)
             if s != nwhip.NW_OK:
@@ -119,10 +141,14 @@ def colband_model_ms(n1: int, n2: int, shape) -> float:
     return COLBAND_PACE_NS[shape] * ((strips - 1) * 64 * nc + n2 + 1) * 1e-6
 
 
-def colband_shape(n1: int, n2: int, substrips: int = 0, strip_waves: int = 0):
-    """The strip shape of a column-band fill: the caller's, else the one of the
-    W = 256 shapes whose modelled critical path is shortest (a chain of many strips
+def colband_shape(n1: int, n2: int, substrips: int = 0, strip_waves: int = 0, kernel: int = 0,
+                  nbands: int = 1):
+    """The shape of a column-band fill: the caller's, else for panels the panel
+    that gives each CU one panel of its band (n1 / nbands columns), for strips the
+    W = 256 shape whose modelled critical path is shortest (a chain of many strips
     wants the short hop of (4,1), a short chain the fast pace of (1,4))."""
+    if kernel == nwhip.KERNEL_PANELS:
+        return (substrips, strip_waves) if (substrips or strip_waves) else panel_shape_for(n1 // max(1, nbands))
     if substrips or strip_waves:
         return nwhip.strip_shape(substrips, strip_waves, n1, n2)
     return min(COLBAND_PACE_NS, key=lambda sh: colband_model_ms(n1, n2, sh))
@@ -137,18 +163,18 @@ class LocalColBands:
     resident workers so that all bands are co-resident."""
 
     def __init__(self, n1: int, n2: int, nbands: int, device: int = 0, substrips: int = 0,
-                 strip_waves: int = 0):
+                 strip_waves: int = 0, kernel: int = 0):
         import torch
-        self.n1, self.n2, self.P, self.device = n1, n2, nbands, device
+        self.n1, self.n2, self.P, self.device, self.kernel = n1, n2, nbands, device, kernel
         # one shape for every band (auto: colband_shape)
-        self.substrips, self.strip_waves = colband_shape(n1, n2, substrips, strip_waves)
-        self.layout = [nwhip.colband_layout(n1, n2, nbands, r, self.substrips, self.strip_waves)
+        self.substrips, self.strip_waves = colband_shape(n1, n2, substrips, strip_waves, kernel, nbands)
+        self.layout = [nwhip.colband_layout(n1, n2, nbands, r, self.substrips, self.strip_waves, kernel)
                        for r in range(nbands)]
         self.tables = [nwhip.Context.alloc_table(nc - 1, n2) for _, _, _, nc in self.layout]
         self.feeds = [None] + [nwhip.Feed(n2, device) for _ in range(nbands - 1)]
         self.ctxs = [nwhip.Context(device) for _ in range(nbands)]
         self.streams = [torch.cuda.Stream(device) for _ in range(nbands)]
-        self.waves = max(1, resident_waves(device, self.substrips, self.strip_waves) // nbands)
+        self.waves = max(1, resident_waves(device, self.substrips, self.strip_waves, kernel) // nbands)
         self.tag = 0
 
     def fill(self, d_s1, d_s2, scheme=(1, 0, -1), flags: int = 0, timeout_ms: int = 0) -> int:
@@ -164,7 +190,8 @@ class LocalColBands:
                 feed_in=self.feeds[r].ptr if r > 0 else None,
                 feed_out=self.feeds[r + 1].ptr if r + 1 < self.P else None,
                 tag=self.tag, scheme=scheme, waves=self.waves, stream=st, flags=flags,
-                substrips=self.substrips, strip_waves=self.strip_waves, timeout_ms=timeout_ms)
+                substrips=self.substrips, strip_waves=self.strip_waves, timeout_ms=timeout_ms,
+                kernel=self.kernel)
         for r, st in enumerate(self.streams):
             s = self.ctxs[r].status(st)
             if s != nwhip.NW_OK:
@@ -198,11 +225,115 @@ def _golden(n1: int, n2: int, scheme):
     return g.get(key)
 
 
+def _sweep(args, partition: str, rank: int, world: int, dev: int, scheme) -> dict:
+    """One multi-rank band sweep: `warmup` + `steps` fills enqueued back to back on
+    this rank's stream, halo / feed buffers alternating by launch parity, the
+    producer's stream waiting on the consumer's "done with launch k" link word
+    (nw_link_*) before it rewrites that launch's buffer -- no host round trip
+    between launches.  Returns this rank's measurements (wall time of the timed
+    launches between a barrier + synchronize on both sides)."""
+    import torch
+    import torch.distributed as dist
+
+    cols = partition == "cols"
+    kernel = getattr(args, "kernel", 0)
+    ctx = nwhip.Context(dev)
+    stream = torch.cuda.current_stream()
+    if cols:
+        # column bands (mpi-vert): rank r owns ~col_width columns of every row
+        n1, n2 = world * args.col_width, args.col_rows
+        sub, nc = colband_shape(n1, n2, args.substrips, args.strip_waves, kernel, world)
+        sf, scount, start, ncols = nwhip.colband_layout(n1, n2, world, rank, sub, nc, kernel=kernel)
+        s1 = torch.from_numpy(nwhip.synth(1, n1)).cuda()
+        s2 = torch.from_numpy(nwhip.synth(2, n2)).cuda()
+        table = nwhip.Context.alloc_table(ncols - 1, n2)
+        links_in = [nwhip.Feed(n2, dev) for _ in range(2)] if rank > 0 else None
+        rows = n2 + 1
+    else:
+        # row bands (mpi-horz, BASELINE config 4): rank r owns band_rows rows
+        n1 = args.band_cols
+        n2 = world * args.band_rows
+        rows, start = nwhip.band_layout(n2, world, rank)
+        # synthetic inputs, identical on every rank (seeds 1 / 2); this rank's side chars only
+        s1 = torch.from_numpy(nwhip.synth(1, n1)).cuda()
+        s2 = torch.from_numpy(nwhip.synth(2, n2)[start:start + rows - 1].copy()).cuda()
+        table = nwhip.Context.alloc_table(n1, rows - 1)
+        links_in = [nwhip.Halo(n1, dev) for _ in range(2)] if rank > 0 else None
+        sub, nc = band_shape(n1, rows - 1, args.substrips, args.strip_waves, kernel)
+        ncols = n1 + 1
+    # rank r exports its two incoming buffers and (r < world-1) the link word its
+    # consumer r+1 signals into; rank r maps r+1's buffers and r-1's word
+    link_word = nwhip.Link(dev) if rank + 1 < world else None
+    mine = ([nwhip.ipc_get_handle(b.ptr) for b in links_in] if links_in else None,
+            nwhip.ipc_get_handle(link_word.ptr) if link_word else None)
+    handles = [None] * world
+    dist.all_gather_object(handles, mine)
+    out_bufs = [nwhip.ipc_open_handle(h) for h in handles[rank + 1][0]] if rank + 1 < world else None
+    prod_word = nwhip.ipc_open_handle(handles[rank - 1][1]) if rank > 0 else None
+    waves = args.waves
+    if args.share_gpu and waves == 0:
+        waves = max(1, resident_waves(dev, sub, nc, kernel) // world)
+
+    def launch(k: int, ev=None):
+        """Launch k (tag k >= 1) on this rank's stream, buffers k % 2."""
+        b = k % 2
+        if out_bufs is not None and k >= 3:
+            nwhip.link_wait(link_word.ptr, k - 2, stream)  # consumer done with launch k-2
+        if ev is not None:
+            ev[0].record(stream)
+        kw = dict(tag=k, scheme=scheme, waves=waves, stream=stream, substrips=sub, strip_waves=nc,
+                  kernel=kernel)
+        if cols:
+            ctx.fill_colband(s1, s2, table, world, rank, feed_in=links_in[b].ptr if links_in else None,
+                             feed_out=out_bufs[b] if out_bufs else None, **kw)
+        else:
+            ctx.fill_band(s1, s2, table, halo_in=links_in[b].ptr if links_in else None,
+                          halo_out=out_bufs[b] if out_bufs else None, row0=start, **kw)
+        if ev is not None:
+            ev[1].record(stream)
+        if prod_word is not None:
+            nwhip.link_signal(prod_word, k, stream)  # done reading launch k's buffer
+
+    for k in range(1, args.warmup + 1):
+        launch(k)
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i, e in enumerate(evs):
+        launch(args.warmup + 1 + i, e)
+    torch.cuda.synchronize()
+    dist.barrier()
+    wall = time.perf_counter() - t0
+    status = ctx.status()
+    link_status = link_word.status() if link_word else 0
+    kms = float(np.mean([a.elapsed_time(b) for a, b in evs])) if evs else 0.0
+    score = int(table[rows - 1, ncols - 1].item()) if rank == world - 1 else None
+    dist.barrier()
+    if out_bufs:
+        for x in out_bufs:
+            nwhip.ipc_close_handle(x)
+    if prod_word is not None:
+        nwhip.ipc_close_handle(prod_word)
+    dist.barrier()
+    for x in (links_in or []) + ([link_word] if link_word else []):
+        x.free()
+    ctx.close()
+    del table
+    torch.cuda.empty_cache()
+    return {"wall": wall, "status": status, "link_status": link_status, "kms": kms, "score": score,
+            "n1": n1, "n2": n2, "shape": [sub, nc], "kernel": kernel, "rows": rows, "start": start}
+
+
 def run_bands(args) -> dict | None:
-    """bench.py --gpus N (N > 1) under torch.distributed.run: one rank per GPU, rank r
-    fills band r of an n1 x (N * band_rows) table (weak scaling: per-GPU band fixed;
-    at N = 8 with the defaults this is BASELINE config 4, 512k x 512k).
-    Prints and returns the JSON line on rank 0."""
+    """bench.py --gpus N (N > 1) under torch.distributed.run: one rank per GPU.
+    `value` = row bands (BASELINE config 4, mpi-horz): rank r fills band r of an
+    n1 x (N * band_rows) table (weak scaling: per-GPU band fixed; at N = 8 with the
+    defaults this is 512k x 512k).  The other partition (column bands, mpi-vert:
+    N * col_width columns x col_rows rows) runs after it as `alt_partition` unless
+    --alt-partition none.  Prints and returns the JSON line on rank 0."""
     import torch
     import torch.distributed as dist
 
@@ -216,99 +347,65 @@ def run_bands(args) -> dict | None:
     if not dist.is_initialized():
         dist.init_process_group("gloo", rank=rank, world_size=world)
     scheme = tuple(int(x) for x in args.scheme.split(","))
-    cols = getattr(args, "partition", "rows") == "cols"
-    ctx = nwhip.Context(dev)
-    stream = torch.cuda.current_stream()
-    if cols:
-        # column bands (mpi-vert): rank r owns ~col_width columns of every row
-        n1, n2 = world * args.col_width, args.col_rows
-        sub, nc = colband_shape(n1, n2, args.substrips, args.strip_waves)
-        sf, scount, start, ncols = nwhip.colband_layout(n1, n2, world, rank, sub, nc)
-        s1 = torch.from_numpy(nwhip.synth(1, n1)).cuda()
-        s2 = torch.from_numpy(nwhip.synth(2, n2)).cuda()
-        table = nwhip.Context.alloc_table(ncols - 1, n2)
-        link_in = nwhip.Feed(n2, dev) if rank > 0 else None
-        rows = n2 + 1
-    else:
-        n1 = args.band_cols
-        n2 = world * args.band_rows
-        rows, start = nwhip.band_layout(n2, world, rank)
-        # synthetic inputs, identical on every rank (seeds 1 / 2); this rank's side chars only
-        s1 = torch.from_numpy(nwhip.synth(1, n1)).cuda()
-        s2 = torch.from_numpy(nwhip.synth(2, n2)[start:start + rows - 1].copy()).cuda()
-        table = nwhip.Context.alloc_table(n1, rows - 1)
-        link_in = nwhip.Halo(n1, dev) if rank > 0 else None
-        sub, nc = nwhip.strip_shape(args.substrips, args.strip_waves, n1, rows - 1)
-    # each rank exports its incoming buffer; rank r-1 maps it and stores into it
-    handles = [None] * world
-    dist.all_gather_object(handles, nwhip.ipc_get_handle(link_in.ptr) if link_in else None)
-    link_out = nwhip.ipc_open_handle(handles[rank + 1]) if rank + 1 < world else None
-    waves = args.waves
-    if args.share_gpu and waves == 0:
-        waves = max(1, resident_waves(dev, sub, nc) // world)
-    tag = 0
-
-    def step(ev=None):
-        nonlocal tag
-        tag += 1
-        if ev is not None:
-            ev[0].record(stream)
-        if cols:
-            ctx.fill_colband(s1, s2, table, world, rank, feed_in=link_in.ptr if link_in else None,
-                             feed_out=link_out, tag=tag, scheme=scheme, waves=waves, stream=stream,
-                             substrips=sub, strip_waves=nc)
-        else:
-            ctx.fill_band(s1, s2, table, halo_in=link_in.ptr if link_in else None,
-                          halo_out=link_out, tag=tag, scheme=scheme, waves=waves, stream=stream,
-                          substrips=sub, strip_waves=nc, row0=start)
-        if ev is not None:
-            ev[1].record(stream)
-        torch.cuda.synchronize()
-        # no rank starts launch k+1 (which rewrites its neighbour's halo / feed)
-        # before every rank has finished launch k
-        dist.barrier()
-
-    for _ in range(args.warmup):
-        step()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
-    dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for e in evs:
-        step(e)
-    torch.cuda.synchronize()
-    dist.barrier()
-    wall = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
-    dist.all_reduce(wall, op=dist.ReduceOp.MAX)
-    status = ctx.status()
-    kms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
-    st_all = [None] * world
-    dist.all_gather_object(st_all, (status, kms, rows, start))
-    last_col = (ncols - 1) if cols else n1
-    score = int(table[rows - 1, last_col].item()) if rank == world - 1 else None
-    scores = [None] * world
-    dist.all_gather_object(scores, score)
-    if link_out is not None:
-        nwhip.ipc_close_handle(link_out)
-    dist.barrier()
-    if link_in is not None:
-        link_in.free()
-    ctx.close()
-    if any(s[0] != 0 for s in st_all):
-        raise RuntimeError(f"band status per rank: {[s[0] for s in st_all]}")
+    main = getattr(args, "partition", "rows")
+    alt = getattr(args, "alt_partition", None)
+    if alt is None:
+        alt = "cols" if main == "rows" else "rows"
+    legs = {}
+    for part in [main] + ([alt] if alt not in ("none", main) else []):
+        m = _sweep(args, part, rank, world, dev, scheme)
+        allm = [None] * world
+        dist.all_gather_object(allm, m)
+        legs[part] = allm
     if rank != 0:
         return None
-    score = scores[-1]
+    out = _line(args, world, scheme, main, legs[main])
+    if alt in legs:
+        a = _line(args, world, scheme, alt, legs[alt])
+        out["alt_partition"] = {k: a[k] for k in ("value", "ms_per_step", "config", "score", "score_golden",
+                                                  "score_ok", "roofline")}
+    if cpu_baseline_fn is not None and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline_fn(args.cpu_n, scheme)
+    print(json.dumps(out), flush=True)
+    bad = [(p, [m["status"] for m in legs[p]], [m["link_status"] for m in legs[p]]) for p in legs
+           if any(m["status"] != 0 or m["link_status"] != 0 for m in legs[p])]
+    if bad:
+        raise RuntimeError(f"band status per rank (fill, link): {bad}")
+    return out
+
+
+cpu_baseline_fn = None  # bench.py installs its cpu_baseline (rank 0 only reports it)
+
+
+def _line(args, world: int, scheme, part: str, ms: list) -> dict:
+    """The bench JSON line of one partition from every rank's _sweep result."""
+    cols = part == "cols"
+    m0, ml = ms[0], ms[-1]
+    n1, n2 = m0["n1"], m0["n2"]
+    wall_s = max(m["wall"] for m in ms)  # max over ranks
+    score = ml["score"]
     want = _golden(n1, n2, scheme)
-    wall_s = float(wall.item())
     cells = n1 * n2
     ms_step = wall_s / args.steps * 1e3
     value = cells * args.steps / wall_s / 1e9
     table_bytes = 4.0 * (n1 + 1) * (n2 + 1)
     per_gpu_bytes = table_bytes / world
     achieved = per_gpu_bytes / (ms_step * 1e6)  # GB/s per GPU, whole step (incl. pipeline ramp)
-    out = {
+    kern = {0: "auto", 1: "strips", 2: "panels"}[m0["kernel"]]
+    common = {"n1": n1, "n2": n2, "scheme": list(scheme), "bands": world, "table_bytes": int(table_bytes),
+              "kernel": kern, "shape": m0["shape"], "control_plane": "torch.distributed gloo (setup, barriers)",
+              "launches": "back to back, buffers by launch parity, link-word flow control (nw_link_*)",
+              "shared_gpu": bool(args.share_gpu)}
+    if cols:
+        cfg = {"workload": f"nw_fill_colbands_{n2}x{n1}", "col_width": args.col_width,
+               "parallelism": f"column bands x{world} (mpi-vert)",
+               "halo": "in-kernel xGMI peer stores of the band's right column, 16 rows at a time", **common}
+    else:
+        cfg = {"workload": f"nw_fill_rowbands_{n2}x{n1}", "band_rows": args.band_rows,
+               "parallelism": f"row bands x{world} (mpi-horz, BASELINE config 4)",
+               "halo": "in-kernel xGMI peer stores of the band's last row, as each strip/panel finishes",
+               **common}
+    return {
         "metric": "GCUPS (DP cell updates/s) on NxN NW fill, bit-exact score",
         "value": round(value, 2),
         "unit": "GCUPS",
@@ -321,29 +418,14 @@ def run_bands(args) -> dict | None:
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic (i.i.d. uniform {1,2,3,4}, seeds 1/2)",
-        "config": ({"workload": f"nw_fill_colbands_{n2}x{n1}", "n1": n1, "n2": n2,
-                    "scheme": list(scheme), "col_width": args.col_width, "bands": world,
-                    "table_bytes": int(table_bytes), "parallelism": f"column bands x{world}",
-                    "halo": "in-kernel xGMI peer stores of the band's right column, 64 rows at a time",
-                    "strip_shape": [sub, nc],
-                    "control_plane": "torch.distributed gloo",
-                    "shared_gpu": bool(args.share_gpu)} if cols else
-                   {"workload": f"nw_fill_rowbands_{n2}x{n1}", "n1": n1, "n2": n2,
-                    "scheme": list(scheme), "band_rows": args.band_rows, "bands": world,
-                    "table_bytes": int(table_bytes), "parallelism": f"row bands x{world}",
-                    "halo": f"in-kernel xGMI peer stores, one strip ({64 * sub * nc} columns) at a time",
-                    "strip_shape": [sub, nc],
-                    "control_plane": "torch.distributed gloo",
-                    "shared_gpu": bool(args.share_gpu)}),
+        "config": cfg,
         "score": score,
         "score_golden": want,
         "score_ok": (want == score) if want is not None else None,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                     "traffic": None, "basis": "per GPU: band table bytes / ms_per_step",
-                     "kernel_ms_avg_per_rank": [round(s[1], 3) for s in st_all]},
+                     "traffic": None, "basis": "per GPU: band table bytes / ms_per_step (whole step)",
+                     "kernel_ms_avg_per_rank": [round(m["kms"], 3) for m in ms]},
         "cpu_baseline": None,
         "kernel": nwhip.version(),
     }
-    print(json.dumps(out), flush=True)
-    return out

@@ -23,16 +23,19 @@ LIB_PATH = os.environ.get("NWHIP_LIB") or os.path.join(HERE, "build", "libnwhip.
 
 NW_OK, NW_ERR_ARG, NW_ERR_HIP, NW_ERR_OOM, NW_ERR_TIMEOUT, NW_ERR_NODEVICE, NW_ERR_UNSUPPORTED = range(7)
 MODE_NW, MODE_SW = 0, 1  # nw_params.mode: global (the reference fills) / Smith-Waterman local
+# nw_params.kernel: auto / anti-diagonal strips (nw_fill.hip) / row-scan panels (nw_rows.hip)
+KERNEL_AUTO, KERNEL_STRIPS, KERNEL_PANELS = 0, 1, 2
 
 # every symbol include/nw_hip.h declares (checked by tests/test_host.py)
 EXPORTS = ["nw_params_default", "nw_strerror", "nw_version", "nw_fill", "nw_table_pitch",
-           "nw_table_bytes", "nw_table_offset", "nw_strip_lds_bytes", "nw_ctx_create", "nw_ctx_destroy", "nw_ctx_workspace_bytes",
+           "nw_table_bytes", "nw_table_offset", "nw_strip_lds_bytes", "nw_panel_lds_bytes", "nw_ctx_create", "nw_ctx_destroy", "nw_ctx_workspace_bytes",
            "nw_fill_device", "nw_fill_device_async", "nw_ctx_status", "nw_read_bdna", "nw_free",
            "nw_synth_bdna", "nw_band_layout", "nw_halo_bytes", "nw_fill_band_async",
            "nw_ipc_get_handle", "nw_ipc_open_handle", "nw_ipc_close_handle", "nw_halo_alloc",
            "nw_halo_free", "nw_fill_emb", "nw_sw_align", "nw_sw_traceback", "nw_tuned_shape", "nw_debug_ctrl", "nw_debug_set_trace",
            "nw_debug_trace_words", "nw_colband_layout", "nw_feed_bytes", "nw_feed_alloc",
-           "nw_fill_colband_async"]
+           "nw_fill_colband_async", "nw_link_alloc", "nw_link_wait_async", "nw_link_signal_async",
+           "nw_link_status"]
 IPC_HANDLE_BYTES = 64
 
 
@@ -40,7 +43,8 @@ class NwParams(ctypes.Structure):
     _fields_ = [("match", ctypes.c_int32), ("mismatch", ctypes.c_int32), ("gap", ctypes.c_int32),
                 ("mode", ctypes.c_int32), ("waves", ctypes.c_int32), ("device", ctypes.c_int32),
                 ("flags", ctypes.c_int32), ("substrips", ctypes.c_int32),
-                ("strip_waves", ctypes.c_int32), ("timeout_ms", ctypes.c_int32)]
+                ("strip_waves", ctypes.c_int32), ("timeout_ms", ctypes.c_int32),
+                ("kernel", ctypes.c_int32)]
 
 
 class NwResult(ctypes.Structure):
@@ -48,7 +52,8 @@ class NwResult(ctypes.Structure):
                 ("kernel_ms", ctypes.c_double), ("table_bytes", ctypes.c_double),
                 ("strips", ctypes.c_int32), ("waves", ctypes.c_int32),
                 ("substrips", ctypes.c_int32), ("strip_waves", ctypes.c_int32),
-                ("end_i", ctypes.c_int64), ("end_j", ctypes.c_int64)]
+                ("end_i", ctypes.c_int64), ("end_j", ctypes.c_int64),
+                ("kernel", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 class NwAlignment(ctypes.Structure):
@@ -121,6 +126,8 @@ def lib() -> ctypes.CDLL:
     L.nw_table_offset.restype = ctypes.c_int64
     L.nw_strip_lds_bytes.argtypes = [ctypes.c_int32, ctypes.c_int32]
     L.nw_strip_lds_bytes.restype = ctypes.c_int64
+    L.nw_panel_lds_bytes.argtypes = [ctypes.c_int32, ctypes.c_int32]
+    L.nw_panel_lds_bytes.restype = ctypes.c_int64
     L.nw_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
     L.nw_ctx_destroy.argtypes = [ctypes.c_void_p]
     L.nw_ctx_destroy.restype = None
@@ -162,6 +169,10 @@ def lib() -> ctypes.CDLL:
     L.nw_fill_colband_async.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
                                         ctypes.c_int64, ctypes.POINTER(NwParams), ctypes.POINTER(NwColBand),
                                         ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+    L.nw_link_alloc.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+    L.nw_link_wait_async.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int32, ctypes.c_void_p]
+    L.nw_link_signal_async.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
+    L.nw_link_status.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32)]
     L.nw_debug_ctrl.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32)]
     L.nw_debug_set_trace.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     L.nw_debug_trace_words.argtypes = []
@@ -190,7 +201,8 @@ class Scheme:
 
 
 def params(scheme=(1, 0, -1), waves: int = 0, device: int = -1, flags: int = 0,
-           substrips: int = 0, strip_waves: int = 0, timeout_ms: int = 0, mode: int = MODE_NW) -> NwParams:
+           substrips: int = 0, strip_waves: int = 0, timeout_ms: int = 0, mode: int = MODE_NW,
+           kernel: int = KERNEL_AUTO) -> NwParams:
     if isinstance(scheme, Scheme):
         scheme = (scheme.match, scheme.mismatch, scheme.gap)
     p = NwParams()
@@ -203,16 +215,18 @@ def params(scheme=(1, 0, -1), waves: int = 0, device: int = -1, flags: int = 0,
     p.strip_waves = int(strip_waves)
     p.timeout_ms = int(timeout_ms)
     p.mode = int(mode)
+    p.kernel = int(kernel)
     return p
 
 
-def sw_align(s1, s2, scheme=(1, -1, -1), device: int = -1, substrips: int = 0, strip_waves: int = 0):
+def sw_align(s1, s2, scheme=(1, -1, -1), device: int = -1, substrips: int = 0, strip_waves: int = 0,
+             kernel: int = KERNEL_AUTO):
     """Smith-Waterman local alignment on the device (nw_sw_align): returns
     (NwAlignment, ops) with ops a uint8 array in path order (0 diag, 1 up, 2 left)."""
     a, b = _seq(s1), _seq(s2)
     ops = np.empty(a.size + b.size + 1, dtype=np.uint8)
     out = NwAlignment()
-    p = params(scheme, device=device, substrips=substrips, strip_waves=strip_waves, mode=MODE_SW)
+    p = params(scheme, device=device, substrips=substrips, strip_waves=strip_waves, mode=MODE_SW, kernel=kernel)
     st = lib().nw_sw_align(a.ctypes.data_as(_i8p), a.size, b.ctypes.data_as(_i8p), b.size, ctypes.byref(p),
                            ops.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), ops.size, ctypes.byref(out))
     if st != NW_OK:
@@ -230,12 +244,12 @@ FLAG_TIMING_ONLY, FLAG_NO_PROFILE = 1, 2  # nw_params.flags (include/nw_hip.h)
 
 
 def fill(s1, s2, scheme=(1, 0, -1), waves: int = 0, device: int = -1, substrips: int = 0,
-         flags: int = 0, strip_waves: int = 0):
+         flags: int = 0, strip_waves: int = 0, kernel: int = KERNEL_AUTO):
     """Full table in the reference layout ((n2+1) x (n1+1) int32) + NwResult."""
     a, b = _seq(s1), _seq(s2)
     t = np.empty((b.size + 1, a.size + 1), dtype=np.int32)
     r = NwResult()
-    p = params(scheme, waves, device, flags=flags, substrips=substrips, strip_waves=strip_waves)
+    p = params(scheme, waves, device, flags=flags, substrips=substrips, strip_waves=strip_waves, kernel=kernel)
     st = lib().nw_fill(a.ctypes.data_as(_i8p), a.size, b.ctypes.data_as(_i8p), b.size,
                        ctypes.byref(p), t.ctypes.data_as(_i32p), ctypes.byref(r))
     if st != NW_OK:
@@ -244,10 +258,10 @@ def fill(s1, s2, scheme=(1, 0, -1), waves: int = 0, device: int = -1, substrips:
 
 
 def score(s1, s2, scheme=(1, 0, -1), waves: int = 0, device: int = -1, substrips: int = 0,
-          strip_waves: int = 0) -> int:
+          strip_waves: int = 0, kernel: int = KERNEL_AUTO) -> int:
     a, b = _seq(s1), _seq(s2)
     r = NwResult()
-    p = params(scheme, waves, device, substrips=substrips, strip_waves=strip_waves)
+    p = params(scheme, waves, device, substrips=substrips, strip_waves=strip_waves, kernel=kernel)
     st = lib().nw_fill(a.ctypes.data_as(_i8p), a.size, b.ctypes.data_as(_i8p), b.size,
                        ctypes.byref(p), None, ctypes.byref(r))
     if st != NW_OK:
@@ -298,6 +312,11 @@ def strip_lds_bytes(substrips: int, strip_waves: int) -> int:
     return int(lib().nw_strip_lds_bytes(substrips, strip_waves))
 
 
+def panel_lds_bytes(substrips: int, strip_waves: int) -> int:
+    """LDS bytes of one panel workgroup of this shape (-1: unsupported shape)."""
+    return int(lib().nw_panel_lds_bytes(substrips, strip_waves))
+
+
 def read_bdna(path: str) -> np.ndarray:
     """readSequence semantics (src/common/helper.cpp:3-25)."""
     buf = _i8p()
@@ -318,12 +337,13 @@ def band_layout(n2: int, nbands: int, r: int):
     return int(rows.value), int(start.value)
 
 
-def colband_layout(n1: int, n2: int, nbands: int, r: int, substrips: int = 0, strip_waves: int = 0):
+def colband_layout(n1: int, n2: int, nbands: int, r: int, substrips: int = 0, strip_waves: int = 0,
+                   kernel: int = KERNEL_AUTO):
     """(strip_first, strip_count, start, n_cols) of column band r: its strips of the
     whole table's sweep and the global columns [start, start + n_cols) of its local
     table, local column 0 = band r-1's last column (src/mpi/mpi-vert.cpp:17,
     mpi-vert-driver.cpp:35-36, at strip granularity)."""
-    p = params(substrips=substrips, strip_waves=strip_waves)
+    p = params(substrips=substrips, strip_waves=strip_waves, kernel=kernel)
     out = [ctypes.c_int64() for _ in range(4)]
     st = lib().nw_colband_layout(n1, n2, nbands, r, ctypes.byref(p), *[ctypes.byref(x) for x in out])
     if st != NW_OK:
@@ -370,6 +390,41 @@ class Feed(Halo):
         if st != NW_OK:
             raise NwError(st, "nw_feed_alloc")
         self.ptr, self.n2 = int(ptr.value), n2
+
+
+class Link(Halo):
+    """A zeroed launch-to-launch flow-control word pair (nw_link_alloc): the
+    consumer band signals into it (peer store), the producer's stream waits on it."""
+
+    def __init__(self, device: int = -1):
+        ptr = ctypes.c_void_p()
+        st = lib().nw_link_alloc(device, ctypes.byref(ptr))
+        if st != NW_OK:
+            raise NwError(st, "nw_link_alloc")
+        self.ptr = int(ptr.value)
+
+    def status(self) -> int:
+        out = ctypes.c_uint32()
+        st = lib().nw_link_status(ctypes.c_void_p(self.ptr), ctypes.byref(out))
+        if st != NW_OK:
+            raise NwError(st, "nw_link_status")
+        return int(out.value)
+
+
+def link_wait(ptr: int, value: int, stream, timeout_ms: int = 0) -> None:
+    """Stream-ordered wait until the link word at `ptr` is >= value (nw_link_wait_async)."""
+    st = lib().nw_link_wait_async(ctypes.c_void_p(ptr), int(value) & 0xFFFFFFFF, int(timeout_ms),
+                                  ctypes.c_void_p(stream.cuda_stream))
+    if st != NW_OK:
+        raise NwError(st, "nw_link_wait_async")
+
+
+def link_signal(ptr: int, value: int, stream) -> None:
+    """Stream-ordered store of `value` into the link word at `ptr` (may be peer memory)."""
+    st = lib().nw_link_signal_async(ctypes.c_void_p(ptr), int(value) & 0xFFFFFFFF,
+                                    ctypes.c_void_p(stream.cuda_stream))
+    if st != NW_OK:
+        raise NwError(st, "nw_link_signal_async")
 
 
 def ipc_get_handle(ptr: int) -> bytes:
@@ -441,7 +496,7 @@ class Context:
 
     def fill(self, d_s1, d_s2, table, scheme=(1, 0, -1), waves: int = 0, stream=None,
              sync: bool = True, flags: int = 0, substrips: int = 0, strip_waves: int = 0,
-             timeout_ms: int = 0, mode: int = MODE_NW):
+             timeout_ms: int = 0, mode: int = MODE_NW, kernel: int = KERNEL_AUTO):
         """d_s1/d_s2: int8/uint8 CUDA tensors; table: from alloc_table.  Returns NwResult
         when sync, else None (launch only)."""
         import torch
@@ -451,7 +506,7 @@ class Context:
         if stream is None:
             stream = torch.cuda.current_stream(table.device)
         sp = ctypes.c_void_p(stream.cuda_stream)
-        p = params(scheme, waves, self.device, flags, substrips, strip_waves, timeout_ms, mode)
+        p = params(scheme, waves, self.device, flags, substrips, strip_waves, timeout_ms, mode, kernel)
         args = (self._h, ctypes.c_void_p(d_s1.data_ptr() if n1 else 0), n1,
                 ctypes.c_void_p(d_s2.data_ptr() if n2 else 0), n2, ctypes.byref(p),
                 ctypes.c_void_p(table.data_ptr()), table.shape[1], sp)
@@ -469,7 +524,7 @@ class Context:
     def fill_band(self, d_s1, d_s2_band, table, halo_in=None, halo_out=None, tag: int = 1,
                   scheme=(1, 0, -1), waves: int = 0, stream=None, flags: int = 0,
                   substrips: int = 0, strip_waves: int = 0, row0: int = 0,
-                  timeout_ms: int = 0) -> None:
+                  timeout_ms: int = 0, kernel: int = KERNEL_AUTO) -> None:
         """Launch one row band (asynchronous).  d_s2_band: the band's side
         characters (len = band rows - 1); table: alloc_table(n1, len(d_s2_band)),
         row 0 = the halo row, global row `row0` (nw_band_layout start).  halo_in /
@@ -490,7 +545,7 @@ class Context:
         if stream is None:
             stream = torch.cuda.current_stream(table.device)
         b = NwBand(addr(halo_in), addr(halo_out), int(tag), int(row0))
-        p = params(scheme, waves, self.device, flags, substrips, strip_waves, timeout_ms)
+        p = params(scheme, waves, self.device, flags, substrips, strip_waves, timeout_ms, kernel=kernel)
         st = lib().nw_fill_band_async(self._h, ctypes.c_void_p(d_s1.data_ptr() if n1 else 0), n1,
                                       ctypes.c_void_p(d_s2_band.data_ptr() if n2 else 0), n2,
                                       ctypes.byref(p), ctypes.byref(b),
@@ -501,7 +556,8 @@ class Context:
 
     def fill_colband(self, d_s1, d_s2, table, nbands: int, r: int, feed_in=None, feed_out=None,
                      tag: int = 1, scheme=(1, 0, -1), waves: int = 0, stream=None, flags: int = 0,
-                     substrips: int = 0, strip_waves: int = 0, timeout_ms: int = 0) -> None:
+                     substrips: int = 0, strip_waves: int = 0, timeout_ms: int = 0,
+                     kernel: int = KERNEL_AUTO) -> None:
         """Launch column band r of nbands (asynchronous).  d_s1 / d_s2: the WHOLE
         sequences; table: alloc_table(n_cols - 1, n2) for the band's colband_layout
         n_cols; feed_in / feed_out: Feed buffers' addresses (raw ints, e.g. peer
@@ -512,7 +568,7 @@ class Context:
         if stream is None:
             stream = torch.cuda.current_stream(table.device)
         b = NwColBand(feed_in, feed_out, int(tag), int(nbands), int(r), 0)
-        p = params(scheme, waves, self.device, flags, substrips, strip_waves, timeout_ms)
+        p = params(scheme, waves, self.device, flags, substrips, strip_waves, timeout_ms, kernel=kernel)
         st = lib().nw_fill_colband_async(self._h, ctypes.c_void_p(d_s1.data_ptr() if n1 else 0), n1,
                                          ctypes.c_void_p(d_s2.data_ptr() if n2 else 0), n2, ctypes.byref(p),
                                          ctypes.byref(b), ctypes.c_void_p(table.data_ptr()), table.shape[1],

@@ -53,6 +53,20 @@ enum {
                                 v_perm score tables */
 };
 
+/* nw_params.kernel: which gfx950 kernel family fills the table.  Both compute
+ * the same cells (serial.cpp:21-33); they differ in how the wavefront maps onto
+ * a wave:
+ *   STRIPS: a wave holds an ANTI-DIAGONAL of a 64*C-column strip (lane = row
+ *           offset; DPP carries the left neighbour), rows leave through a
+ *           128-slot LDS ring.  Shapes (substrips C, strip_waves NC): (4,1)
+ *           (2,1) (1,1) (2,2) (1,2) (1,4).
+ *   PANELS: a wave holds a ROW of 64*C columns, computed as a prefix maximum
+ *           (lane-local prefix + a 64-lane DPP max-scan) in the w form; rows
+ *           leave through a 32-row ring.  Shapes (C, NW compute waves per
+ *           panel): (4,4) (2,8) (4,2) (2,4) (4,1) (2,2) (1,4) (1,8).
+ *   AUTO:   the measured choice for the table size (nw_tuned_shape). */
+enum { NW_KERNEL_AUTO = 0, NW_KERNEL_STRIPS = 1, NW_KERNEL_PANELS = 2 };
+
 /* Runtime replacement for the compile-time constants of
  * src/common/needleman-wunsch.hpp:11-13 (MATCH 1, MISMATCH 0, GAP -1). */
 typedef struct nw_params {
@@ -71,6 +85,9 @@ typedef struct nw_params {
     int32_t timeout_ms;  /* bound of every in-kernel wait (hand-off, halo, ring);
                             0 = 20000.  A wait that expires makes the fill return
                             NW_ERR_TIMEOUT instead of hanging the device. */
+    int32_t kernel;      /* NW_KERNEL_*; 0 = auto.  With PANELS, substrips /
+                            strip_waves are the panel's (C, NW): a panel is
+                            NW * 64 * C columns */
 } nw_params;
 
 typedef struct nw_result {
@@ -85,6 +102,8 @@ typedef struct nw_result {
     int32_t strip_waves;    /* compute waves per strip                    */
     int64_t end_i, end_j;   /* cell `score` was read from: (n2, n1) for NW; for SW
                                the best cell, first in row-major order     */
+    int32_t kernel;         /* NW_KERNEL_STRIPS or NW_KERNEL_PANELS (what ran) */
+    int32_t reserved;
 } nw_result;
 
 /* A Smith-Waterman alignment (nw_sw_align / nw_sw_traceback). */
@@ -171,6 +190,9 @@ int64_t nw_table_offset(void);
  * caller co-scheduling several fills on one device (LocalBands) sizes their
  * `waves` from it so that all of them stay resident. */
 int64_t nw_strip_lds_bytes(int32_t substrips, int32_t strip_waves);
+/* LDS bytes of one PANEL workgroup (NW_KERNEL_PANELS) of shape (C, NW); -1 if
+ * unsupported. */
+int64_t nw_panel_lds_bytes(int32_t substrips, int32_t strip_waves);
 
 /* Create / destroy a context bound to `device` (-1 = current).  The context
  * owns the hand-off workspace and the strip ticket counter. */
@@ -294,6 +316,26 @@ int nw_fill_colband_async(nw_ctx *ctx, const int8_t *d_s1, int64_t n1, const int
 int nw_ipc_get_handle(const void *d_ptr, void *handle);
 int nw_ipc_open_handle(const void *handle, void **d_ptr);
 int nw_ipc_close_handle(void *d_ptr);
+
+/* Launch-to-launch flow control between neighbouring bands -------------------
+ * A band sweep that enqueues K fills back to back (no host round trip between
+ * them) alternates two halo / feed buffers by launch parity, so the producer's
+ * launch k + 2 must not start before the consumer's launch k has read buffer
+ * k % 2.  The consumer signals "done with launch k" into a LINK word that lives
+ * in the producer's memory (a peer store over xGMI), the producer's stream waits
+ * on it.  (The reference's blocking MPI_Send / MPI_Recv pairs,
+ * src/mpi/mpi-horz.cpp:41-42,53-54, give the same ordering per chunk.)
+ * nw_link_alloc: a zeroed 256-byte fine-grained word pair of its own allocation
+ *   (exportable by nw_ipc_get_handle; free with nw_halo_free).
+ * nw_link_wait_async: stream-ordered wait until word[0] >= value (wrapping
+ *   compare); after timeout_ms (0 = 20000) it gives up and records value in
+ *   word[1].
+ * nw_link_signal_async: stream-ordered word[0] = value (word may be peer memory).
+ * nw_link_status: word[1] (0 = no wait gave up), read synchronously. */
+int nw_link_alloc(int device, uint32_t **d_word);
+int nw_link_wait_async(uint32_t *d_word, uint32_t value, int32_t timeout_ms, void *stream);
+int nw_link_signal_async(uint32_t *d_word, uint32_t value, void *stream);
+int nw_link_status(const uint32_t *d_word, uint32_t *out);
 
 /* Check the in-kernel watchdog word of the last launch (syncs the stream). */
 int nw_ctx_status(nw_ctx *ctx, void *stream);

@@ -21,6 +21,7 @@ ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--flags", type=int, default=0)
 ap.add_argument("--shapes", default="0:0")
 ap.add_argument("--pitches", default="0")
+ap.add_argument("--kernel", type=int, default=0, help="0 auto, 1 strips, 2 panels")
 args = ap.parse_args()
 ctx = nwhip.Context(0)
 shapes = [tuple(int(v) for v in x.split(":")) for x in args.shapes.split(",")]
@@ -31,7 +32,7 @@ for n in [int(x) for x in args.sizes.split(",")]:
         tab = nwhip.Context.alloc_table(n, n, pitch=pitch)
         for w in [int(x) for x in args.waves.split(",")]:
             for c, nc in shapes:
-                kw = dict(waves=w, flags=args.flags, substrips=c, strip_waves=nc)
+                kw = dict(waves=w, flags=args.flags, substrips=c, strip_waves=nc, kernel=args.kernel)
                 ctx.fill(s1, s2, tab, **kw)  # warmup
                 ts = []
                 for _ in range(args.reps):
@@ -40,7 +41,7 @@ for n in [int(x) for x in args.sizes.split(",")]:
                 ms = min(ts)
                 gcups = n * n / (ms * 1e6)
                 print(f"n={n} pitch={tab.shape[1]} C={r.substrips} NC={r.strip_waves} "
-                      f"waves={r.waves} strips={r.strips} ms={ms:.3f} "
+                      f"kernel={r.kernel} waves={r.waves} strips={r.strips} ms={ms:.3f} "
                       f"(all {[round(t, 3) for t in ts]}) GCUPS={gcups:.1f} "
                       f"store_GBps={4 * (n + 1) * (n + 1) / (ms * 1e6):.1f} score={r.score} "
                       f"status={r.status}", flush=True)
