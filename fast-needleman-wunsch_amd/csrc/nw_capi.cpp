@@ -132,7 +132,7 @@ Shape make_shape(int64_t n1, int64_t n2, int32_t waves_req, int32_t sub_req, int
             panel_auto(n1, cus, &s.K, &s.NC);
         } else {
             s.K = sub_req > 0 ? sub_req : 4;
-            s.NC = nc_req > 0 ? nc_req : (s.K == 4 ? 4 : s.K == 2 ? 8 : 8);
+            s.NC = nc_req > 0 ? nc_req : 4;
         }
     } else if (sub_req <= 0 && nc_req <= 0 && sw) {
         // Smith-Waterman cells cost 4 VALU instead of 2, which moves the balance
@@ -155,7 +155,9 @@ Shape make_shape(int64_t n1, int64_t n2, int32_t waves_req, int32_t sub_req, int
     // panel workgroup is 2 * NW waves: at most 32 waves per CU)
     const int lds = s.kernel == NW_KERNEL_PANELS ? nw::panel_lds_bytes(s.K, s.NC) : nw::lds_bytes(s.K, s.NC);
     int64_t per_cu = std::max(1, kLdsPerCU / std::max(lds, 1));
-    if (s.kernel == NW_KERNEL_PANELS) per_cu = std::min<int64_t>(per_cu, std::max(1, 32 / (2 * s.NC)));
+    // a panel workgroup (NW compute, 2-3 store waves per compute wave, 2 feeder
+    // waves, ~88 VGPRs each) fills a CU's wave slots on its own
+    if (s.kernel == NW_KERNEL_PANELS) per_cu = 1;
     int64_t w = waves_req > 0 ? waves_req : per_cu * cus;
     s.waves_max = std::max<int64_t>(1, w);
     s.waves = std::max<int64_t>(1, std::min<int64_t>(w, s.nstrips));

@@ -36,11 +36,15 @@
 //     always already running (deadlock-free for any grid / residency), the GPU
 //     analogue of idxarray-mt's progress counters (idxarray-mt.cpp:8,44,50-56).
 //   * A workgroup = NW compute waves (wave w: columns w*64C .. +64C-1 of the
-//     panel) + NW store waves (store wave w drains compute wave w's ring).
+//     panel), kSPW store waves per compute wave (batches of its ring dealt
+//     round robin), a feeder-in and a feeder-out wave.  Compute waves touch
+//     only LDS (and s_load the row characters): every global-memory access of
+//     the hand-off sits in a wave of its own, whose stalls stall nobody else.
 //   * Hand-off inside the panel: wave w reads wave w-1's last column straight
-//     out of w-1's ring; between panels: the panel's last wave publishes its
-//     last column as {tag, value} granules in 16-row chunks, the next panel's
-//     first wave polls them into its feed ring (nw_dev.h).
+//     out of w-1's ring; between panels: the feeder-out wave publishes the last
+//     compute wave's last column as {tag, value} granules as rows complete, the
+//     next panel's feeder-in wave polls them (64 rows per load, the leading run
+//     whose tags match) into the feed ring of its first compute wave (nw_dev.h).
 //   * No MFMA: integer max/add with no contraction.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -55,14 +59,13 @@ constexpr int kR = 32;           // ring rows per compute wave (a power of two)
 constexpr int kFeedRows = 256;   // feed ring of a panel's first wave (a power of two)
 constexpr int kG = 4;            // rows per group (one v_perm word): ring / feed checks, counters
 constexpr int kBatch = 8;        // rows per store-wave batch
-constexpr int kChunk = 8;        // rows per hand-off granule chunk
 constexpr int kEnt = 16;         // rows per rowpack entry (16 row characters)
 
 // Store waves per compute wave.  Under full HBM load one 1 KB store holds its
 // wave for ~330 cycles (tools/ubench/panel_store: 4 waves x 1 KB per CU reach
 // 6.3 TB/s), so a single store wave serialises those stalls with its own ring
 // reads; two or three per ring overlap them.  A workgroup stays <= 16 waves.
-constexpr int spw(int nw) { return nw >= 8 ? 1 : nw == 4 ? 2 : 3; }
+constexpr int spw(int nw) { return nw == 4 ? 2 : 3; }
 
 template <int C, int NW>
 struct Lay {
@@ -72,17 +75,21 @@ struct Lay {
     static constexpr int kFeed = NW * kRing;      // byte offset of the feed ring
     static constexpr int kCtl = kFeed + kFeedRows * 4;
     // counters per compute wave w (rows 0 .. v-1 done): [0] written into the
-    // ring, [2] read (left values) by wave w+1, [4 + q] read by its store wave q
+    // ring, [1] (last wave) read by the feeder-out wave, [2] read (left values)
+    // by wave w+1, [4 + q] read by its store wave q
     static constexpr int kSPW = spw(NW);
     static constexpr int kCtlWords = 8;
-    static constexpr int kPanelWord = NW * kCtlWords;  // [+0] ticket, [+1] t[0][0]
+    // panel words: [+0] ticket, [+1] t[0][0], [+2] feed rows in the feed ring
+    // (feeder-in), [+3] feed rows read by wave 0
+    static constexpr int kPanelWord = NW * kCtlWords;
     static constexpr int kBytes = kCtl + (kPanelWord + 4) * 4;
-    static constexpr int kWaves = NW * (1 + kSPW);
+    // NW compute waves, NW * kSPW store waves, the feeder-in and feeder-out waves
+    static constexpr int kFeedIn = NW * (1 + kSPW);
+    static constexpr int kWaves = kFeedIn + 2;
 };
 
 static_assert(Lay<4, 4>::kBytes <= 160 * 1024, "ring must fit a CU's LDS");
-static_assert(Lay<2, 8>::kBytes <= 160 * 1024, "ring must fit a CU's LDS");
-static_assert(Lay<4, 4>::kWaves <= 16 && Lay<2, 8>::kWaves <= 16 && Lay<4, 2>::kWaves <= 16, "1024 threads");
+static_assert(Lay<4, 4>::kWaves <= 16 && Lay<4, 2>::kWaves <= 16 && Lay<4, 1>::kWaves <= 16, "1024 threads");
 
 // Constant address space: uniform loads of the row characters become s_load.
 typedef __attribute__((address_space(4))) const uint32_t cu32;
@@ -205,29 +212,21 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
 
     // ---- the left column, rows 0 .. : x[r][j0-1]
     //   wave w > 0: wave w-1's last column, read out of w-1's ring;
-    //   wave 0 of panel > 0 (or a column band's first panel): granules of the
-    //     previous panel's last wave, polled into this wave's feed ring;
+    //   wave 0 of panel > 0 (or a column band's first panel): the feed ring, which
+    //     the feeder-in wave fills from the previous panel's granules;
     //   wave 0 of panel 0: the boundary column 0 (x = t[0][0] for NW, 0 for SW),
     //     or nothing when the panels start at column 0 (kNeg).
-    enum { SRC_BOUND = 0, SRC_GRAN = 1, SRC_RING = 2 };
-    const bool fed = p == A.strip0 && A.feed_in != nullptr;
-    const bool feeds = p == A.strip0 + A.nstrips - 1 && A.feed_out != nullptr;
-    const int src = w > 0 ? SRC_RING : (p > 0 || fed) ? SRC_GRAN : SRC_BOUND;
+    // Either way an LDS producer with a rows-available counter.
+    enum { SRC_BOUND = 0, SRC_FEED = 1, SRC_RING = 2 };
+    const int src = w > 0 ? SRC_RING : p > 0 ? SRC_FEED : SRC_BOUND;
     const int32_t lbound = j0 >= 1 ? (SW ? 0 : bnd0) : kNeg;
     int32_t *feed = (int32_t *)(lds + L::kFeed);
     // byte address of the left value of row r: base + (r & mask) * stride
     const uint32_t lbase = src == SRC_RING ? (uint32_t)((w - 1) * L::kRing + L::kRowB - 4) : (uint32_t)L::kFeed;
     const uint32_t lstride = src == SRC_RING ? (uint32_t)L::kRowB : 4u;
     const uint32_t lmask = src == SRC_RING ? (uint32_t)(kR - 1) : (uint32_t)(kFeedRows - 1);
-    const int32_t *prod_written = ctl + (w > 0 ? w - 1 : 0) * L::kCtlWords;  // SRC_RING
-    int32_t *my_consumed = ctl + (w > 0 ? w - 1 : 0) * L::kCtlWords + 2;     // SRC_RING
-    // granules: in of the previous panel (slot (p-1) % M) or the left band's feed;
-    // out into slot p % M or the right band's feed
-    const uint64_t *gin = fed ? A.feed_in : A.gran + (int64_t)((p + A.M - 1) % A.M) * A.gstride;
-    uint64_t *gout = feeds ? A.feed_out : A.gran + (int64_t)(p % A.M) * A.gstride;
-    const uint32_t tag_in = fed ? A.feed_tag : A.tagbase + (uint32_t)p;
-    const uint64_t tagw = (uint64_t)(feeds ? A.feed_tag : A.tagbase + (uint32_t)p + 1u) << 32;
-    const bool publishes = w == NW - 1;
+    const int32_t *prod_written = src == SRC_RING ? ctl + (w - 1) * L::kCtlWords : ctl + L::kPanelWord + 2;
+    int32_t *my_consumed = src == SRC_RING ? ctl + (w - 1) * L::kCtlWords + 2 : ctl + L::kPanelWord + 3;
 
     // ---- the ring: row r of this wave at ring + (r & (kR-1)) * kRowB, lane piece 4C bytes
     const uint32_t rlane = (uint32_t)(w * L::kRing) + (uint32_t)lane * (4u * C);
@@ -239,30 +238,35 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
     // Ring space: rows 0 .. need-1 must have left the ring (read by my store wave
     // and, for w < NW-1, by wave w+1).  The counters are loaded one group early
     // (cbv) so that the check waits on nothing in the common case.
-    int32_t cbv = 0;
+    // cbr: the counters as loaded (raw: the minimum is taken at the check, so
+    // that the loads' latency is not waited for where they are issued)
+    int32_t cbr[L::kSPW + 1];
+#pragma unroll
+    for (int q = 0; q <= L::kSPW; ++q) cbr[q] = 0;
     auto ring_space = [&](int32_t need) {
-        int32_t cb = __builtin_amdgcn_readfirstlane(cbv);
+        int32_t v = cbr[0];
+#pragma unroll
+        for (int q = 1; q <= L::kSPW; ++q) v = min(v, cbr[q]);
+        const int32_t cb = __builtin_amdgcn_readfirstlane(v);
         if (cb < need) {
             const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
             bool d = false;
 #pragma unroll
             for (int q = 0; q < L::kSPW; ++q) d |= wait_counter(ctr + 4 + q, need, A.ctrl, 11, tmo) == kDead;
-            if (w + 1 < NW) d |= wait_counter(ctr + 2, need, A.ctrl, 12, tmo) == kDead;
+            d |= wait_counter(ctr + (w + 1 < NW ? 2 : 1), need, A.ctrl, 12, tmo) == kDead;
             dead |= d;
             rticks += __builtin_amdgcn_s_memrealtime() - w0;
         }
         lds_order();  // ring writes after the check
     };
     auto ring_poll = [&]() {
-        int32_t v = ctr_load(ctr + 4);
 #pragma unroll
-        for (int q = 1; q < L::kSPW; ++q) v = min(v, ctr_load(ctr + 4 + q));
-        if (w + 1 < NW) v = min(v, ctr_load(ctr + 2));
-        cbv = v;
+        for (int q = 0; q < L::kSPW; ++q) cbr[q] = ctr_load(ctr + 4 + q);
+        cbr[L::kSPW] = ctr_load(ctr + (w + 1 < NW ? 2 : 1));  // wave w+1 / the feeder-out
     };
 
-    // Left values, SRC_RING: wave w-1 must have written rows 0 .. need-1 (its
-    // counter loaded one group early into fbv).
+    // Left values: the producer (wave w-1 / the feeder-in) must have made rows
+    // 0 .. need-1 available (its counter loaded one group early into fbv).
     int32_t fbv = 0;
     auto ring_feed = [&](int32_t need) {
         int32_t fb = __builtin_amdgcn_readfirstlane(fbv);
@@ -272,25 +276,7 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
             nslow += 1;
             wticks += __builtin_amdgcn_s_memrealtime() - w0;
         }
-        lds_order();  // ring reads after the counter that allowed them
-    };
-    // SRC_GRAN: chunk c (rows 8c .. 8c+7) is loaded by lanes 0..7 (8..15 repeat
-    // them) two chunks ahead into gq[c & 3], checked for its tag when its rows are
-    // first needed (slow path: poll), and copied into the feed ring.
-    uint64_t gq[4] = {0, 0, 0, 0};
-    const int32_t lastc = nrow_it / kChunk - 1;
-    auto gload = [&](int32_t c) -> uint64_t {
-        return gran_load(gin + (int64_t)min(c, lastc) * kChunk + (lane & (kChunk - 1)));
-    };
-    auto feed_chunk = [&](int32_t c, uint64_t g) {
-        if (!__all((lane >= 16) || (uint32_t)(g >> 32) == tag_in)) {
-            const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
-            g = wait_chunk(gin + (int64_t)min(c, lastc) * kChunk + (lane & (kChunk - 1)), tag_in, 0, A.ctrl, 13, tmo);
-            dead |= !__all((lane >= 16) || (uint32_t)(g >> 32) == tag_in);
-            nslow += 1;
-            wticks += __builtin_amdgcn_s_memrealtime() - w0;
-        }
-        if (lane < kChunk) feed[(c * kChunk + lane) & (kFeedRows - 1)] = (int32_t)(uint32_t)g;
+        lds_order();  // reads after the counter that allowed them
     };
     if (src == SRC_BOUND) {
         for (int i = lane; i < kFeedRows; i += kWave) feed[i] = lbound;  // a constant left column
@@ -301,7 +287,7 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
         const uint32_t a = lbase + ((uint32_t)r & lmask) * lstride;
 #pragma unroll
         for (int q = 0; q < kG; ++q) lv[q] = *(const int32_t *)(lds + a + (uint32_t)q * lstride);
-        if (src == SRC_RING) {
+        if (src != SRC_BOUND) {
             lds_order();
             ctr_store(my_consumed, r + kG);  // (in-order LDS: after the reads)
         }
@@ -350,22 +336,12 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
     // (the initial x) goes into the ring without being computed.  The left
     // values of a group are loaded one group ahead.
     int32_t lvA[kG], lvB[kG];
-    uint32_t grow = 0;  // last wave: a chunk's last column, read back for publishing
     wload(0, wd[0]);
     wload(1, wd[1]);
-    if (src == SRC_GRAN) {
-        gq[0] = gload(0);
-        gq[1] = gload(1);
-        feed_chunk(0, gq[0]);
-        gq[2] = gload(2);
-        lds_order();
-    } else if (src == SRC_RING) {
-        ring_feed(kG);
-    }
+    if (src != SRC_BOUND) ring_feed(kG);
     feed_load(0, lvA);
-    if (src == SRC_RING) fbv = ctr_load(prod_written);
+    if (src != SRC_BOUND) fbv = ctr_load(prod_written);
     const uint64_t tstart = __builtin_amdgcn_s_memrealtime();
-    int32_t pend = -1;  // chunk read back into grow, not yet published
     for (int trip = 0; trip < ntrips && !dead; ++trip) {
         static_for<0, 16>([&](auto gc) {
             constexpr int g = decltype(gc)::value;
@@ -380,24 +356,12 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
 #pragma unroll
             for (int k = 0; k < C; ++k) pks[k] = PERM ? __builtin_amdgcn_perm(thi[k], tlo[k], word) : 0u;
             if constexpr ((g & 3) == 0) wload(r0 / kEnt + 2, wd[((g >> 2) + 2) & 3]);
-            if (publishes && pend >= 0) {
-                if (lane < kChunk) gran_store(gout + pend + lane, tagw | grow);
-                pend = -1;
-            }
             // the next group's left values
             const int32_t rn = r0 + kG;
             if (rn < nrow_it) {
-                if (src == SRC_RING) {
-                    ring_feed(rn + kG);
-                } else if (src == SRC_GRAN && (g & 1) == 1) {
-                    constexpr int cs = ((g + 1) >> 1) & 3;  // chunk rn / 8 lives in gq[cs]
-                    feed_chunk(rn / kChunk, gq[cs]);
-                    gq[(cs + 2) & 3] = gload(rn / kChunk + 2);
-                    lds_order();
-                }
+                if (src != SRC_BOUND) ring_feed(rn + kG);
                 feed_load(rn, lvn);
             }
-            if (src == SRC_RING) fbv = ctr_load(prod_written);
 #pragma unroll
             for (int u = 0; u < kG; ++u) {
                 if (!(g == 0 && u == 0) || trip != 0) row(word, pks, u, lv[u]);
@@ -409,26 +373,21 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
                 } else {
                     *(int4 *)dst = make_int4(x[0], x[1], x[2], x[3]);
                 }
+                if (u == 1) {
+                    // counters for the next group's checks, read mid-group so that
+                    // their latency hides behind rows 2 and 3
+                    ring_poll();
+                    if (src != SRC_BOUND) fbv = ctr_load(prod_written);
+                }
             }
             lds_order();
             ctr_store(ctr, r0 + kG);  // rows written
-            ring_poll();              // for the next group's check
-            if (publishes && (g & 1) == 1) {
-                // chunk rows r0-4 .. r0+3 complete: read its last column back now,
-                // publish it at the next group (the LDS latency hides behind it)
-                const int32_t c0 = r0 + kG - kChunk;
-                grow = *(const uint32_t *)(lds + (uint32_t)(w * L::kRing) +
-                                           (uint32_t)((c0 + (lane & (kChunk - 1))) & (kR - 1)) * L::kRowB +
-                                           L::kRowB - 4);
-                pend = c0;
-            }
         });
     }
-    if (publishes && pend >= 0 && lane < kChunk) gran_store(gout + pend + lane, tagw | grow);
     // every row is in the ring (or the panel is abandoned): release the store
-    // wave and the neighbour waves
+    // waves, the feeder-out and the neighbour waves
     ctr_store(ctr, kDone);
-    if (src == SRC_RING) ctr_store(my_consumed, kDone);
+    if (src != SRC_BOUND) ctr_store(my_consumed, kDone);
     if (A.trace != nullptr && lane == 0) {
         uint64_t *tr = A.trace + (int64_t)(p - A.strip0) * kTraceWords;
         if (w == 0) {
@@ -444,6 +403,87 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
         }
     }
     (void)nrows;
+}
+
+// Feeder-in wave of panel p > 0: polls the previous panel's granules (or a
+// column band's feed) 64 rows per load and appends the leading run whose tags
+// match this launch to the feed ring of compute wave 0, publishing rows
+// available in the panel word [+2].  Bounded: gives up (error word) after the
+// watchdog interval without progress.
+template <int C, int NW>
+__device__ __forceinline__ void feeder_in(const FillArgs &A, char *__restrict__ lds, int p, int lane) {
+    typedef Lay<C, NW> L;
+    if (p == 0) return;  // panel 0's left column is the boundary
+    int32_t *ctl = (int32_t *)(lds + L::kCtl);
+    int32_t *avail_w = ctl + L::kPanelWord + 2;
+    const int32_t *cons = ctl + L::kPanelWord + 3;
+    int32_t *feed = (int32_t *)(lds + L::kFeed);
+    const bool fed = p == A.strip0 && A.feed_in != nullptr;
+    const uint64_t *gin = fed ? A.feed_in : A.gran + (int64_t)((p + A.M - 1) % A.M) * A.gstride;
+    const uint32_t tag_in = fed ? A.feed_tag : A.tagbase + (uint32_t)p;
+    const int32_t nrow_it = 64 * A.nblocks;
+    const uint64_t tmo = A.timeout_ticks;
+    int32_t avail = 0, consv = 0;
+    uint64_t t_last = __builtin_amdgcn_s_memrealtime();
+    while (avail < nrow_it) {
+        // feed-ring space for rows avail .. avail+63
+        const int32_t need = avail + kWave - kFeedRows;
+        if (consv < need) {
+            consv = wait_counter(cons, need, A.ctrl, 16, tmo);
+            if (consv == kDead) break;
+        }
+        const int32_t r = avail + lane;
+        const uint64_t g = gran_load(gin + min(r, nrow_it - 1));
+        const uint64_t ok = __ballot(r < nrow_it && (uint32_t)(g >> 32) == tag_in);
+        const int n = ok == ~0ull ? 64 : (int)__builtin_ctzll(~ok);  // leading run
+        if (n > 0) {
+            if (lane < n) feed[(uint32_t)r & (kFeedRows - 1)] = (int32_t)(uint32_t)g;
+            lds_order();
+            avail += n;
+            ctr_store(avail_w, avail);
+            t_last = __builtin_amdgcn_s_memrealtime();
+        } else {
+            if (ctrl_load(A.ctrl + 1) != 0u) break;
+            if (__builtin_amdgcn_s_memrealtime() - t_last > tmo) {
+                give_up(A.ctrl, 1u, 13, gin + min(avail, nrow_it - 1), tag_in, (int64_t)(g >> 32));
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    ctr_store(avail_w, kDone);
+}
+
+// Feeder-out wave: publishes the last compute wave's last column, rows 0 .. as
+// they complete (up to 32 per store, one {tag, value} granule per row), into
+// this panel's granule slot (or a column band's feed, peer memory), and
+// releases those ring rows (counter [1] of the last wave).
+template <int C, int NW>
+__device__ __forceinline__ void feeder_out(const FillArgs &A, char *__restrict__ lds, int p, int lane) {
+    typedef Lay<C, NW> L;
+    int32_t *ctl = (int32_t *)(lds + L::kCtl);
+    int32_t *ctr_l = ctl + (NW - 1) * L::kCtlWords;
+    const bool feeds = p == A.strip0 + A.nstrips - 1 && A.feed_out != nullptr;
+    uint64_t *gout = feeds ? A.feed_out : A.gran + (int64_t)(p % A.M) * A.gstride;
+    const uint64_t tagw = (uint64_t)(feeds ? A.feed_tag : A.tagbase + (uint32_t)p + 1u) << 32;
+    const int32_t nrow_it = 64 * A.nblocks;
+    const uint32_t lastcol = (uint32_t)((NW - 1) * L::kRing + L::kRowB - 4);
+    int32_t pub = 0;
+    while (pub < nrow_it) {
+        int32_t wr = __builtin_amdgcn_readfirstlane(ctr_load(ctr_l));
+        if (wr != kDone && wr <= pub) wr = wait_counter(ctr_l, pub + 1, A.ctrl, 17, A.timeout_ticks);
+        if (wr == kDead) break;
+        lds_order();
+        const int32_t hi = wr == kDone ? nrow_it : min(wr, nrow_it);
+        const int32_t n = min(hi - pub, kR);
+        uint32_t v = 0;
+        if (lane < n) v = *(const uint32_t *)(lds + lastcol + (uint32_t)((pub + lane) & (kR - 1)) * L::kRowB);
+        lds_order();
+        ctr_store(ctr_l + 1, pub + n);  // ring rows released (in-order LDS: after the reads)
+        if (lane < n) gran_store(gout + pub + lane, tagw | v);
+        pub += n;
+    }
+    ctr_store(ctr_l + 1, kDone);
 }
 
 // SW: fold a store wave's running maximum into the panel's word A.smax[p].
@@ -585,9 +625,17 @@ __global__ __launch_bounds__((64 * Lay<C, NW>::kWaves)) void nw_fill_panels(Fill
     int32_t *ctl = (int32_t *)(lds + L::kCtl);
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // issue priority: the compute waves are the latency-bound chain (their
+    // partners on a SIMD are store waves, whose stalls are the memory's)
+#ifndef NW_PANEL_NOPRIO
+    if (wave < NW)
+        __builtin_amdgcn_s_setprio(2);
+    else if (wave >= L::kFeedIn)
+        __builtin_amdgcn_s_setprio(1);
+#endif
     for (;;) {
         if (threadIdx.x == 0) {
-            for (int w = 0; w < L::kPanelWord; ++w) ctl[w] = 0;
+            for (int w = 0; w < L::kPanelWord + 4; ++w) ctl[w] = 0;  // (the panel words too)
             ctl[L::kPanelWord] = (int32_t)atomicAdd(A.ctrl, 1u);
         }
         __syncthreads();
@@ -608,9 +656,13 @@ __global__ __launch_bounds__((64 * Lay<C, NW>::kWaves)) void nw_fill_panels(Fill
                 else
                     compute_panel<C, NW, SUB_GEN>(A, lds, p, wave, lane);
             }
-        } else {
+        } else if (wave < L::kFeedIn) {
             const int b = wave - NW;  // store wave b / NW of ring b % NW
             store_panel<C, NW>(A, lds, p, b % NW, b / NW, lane);
+        } else if (wave == L::kFeedIn) {
+            feeder_in<C, NW>(A, lds, p, lane);
+        } else {
+            feeder_out<C, NW>(A, lds, p, lane);
         }
         __syncthreads();  // the rings and counters are reused by the next panel
     }
@@ -626,8 +678,8 @@ __global__ __launch_bounds__((64 * Lay<C, NW>::kWaves)) void nw_fill_panels(Fill
 
 bool panel_shape_ok(int c, int nwaves) {
     switch (c * 16 + nwaves) {
-        case 4 * 16 + 4: case 2 * 16 + 8: case 4 * 16 + 2: case 2 * 16 + 4:
-        case 4 * 16 + 1: case 2 * 16 + 2: case 1 * 16 + 4: case 1 * 16 + 8:
+        case 4 * 16 + 4: case 4 * 16 + 2: case 2 * 16 + 4:
+        case 4 * 16 + 1: case 2 * 16 + 2: case 1 * 16 + 4:
             return NW_PSHAPE(c, nwaves);
         default:
             return false;
@@ -637,13 +689,11 @@ bool panel_shape_ok(int c, int nwaves) {
 int panel_lds_bytes(int c, int nwaves) {
     switch (c * 16 + nwaves) {
         case 4 * 16 + 4: return rows::Lay<4, 4>::kBytes;
-        case 2 * 16 + 8: return rows::Lay<2, 8>::kBytes;
         case 4 * 16 + 2: return rows::Lay<4, 2>::kBytes;
         case 2 * 16 + 4: return rows::Lay<2, 4>::kBytes;
         case 4 * 16 + 1: return rows::Lay<4, 1>::kBytes;
         case 2 * 16 + 2: return rows::Lay<2, 2>::kBytes;
         case 1 * 16 + 4: return rows::Lay<1, 4>::kBytes;
-        case 1 * 16 + 8: return rows::Lay<1, 8>::kBytes;
         default: return -1;
     }
 }
@@ -663,8 +713,8 @@ int launch_panels(const FillArgs &a, int c, int nwaves, int grid, void *stream) 
     switch (c * 16 + nwaves) {
 #define NW_PCASE(cc, nn) \
         case cc * 16 + nn: if constexpr (NW_PSHAPE(cc, nn)) launch_p<cc, nn>(a, grid, s); break;
-        NW_PCASE(4, 4) NW_PCASE(2, 8) NW_PCASE(4, 2) NW_PCASE(2, 4)
-        NW_PCASE(4, 1) NW_PCASE(2, 2) NW_PCASE(1, 4) NW_PCASE(1, 8)
+        NW_PCASE(4, 4) NW_PCASE(4, 2) NW_PCASE(2, 4)
+        NW_PCASE(4, 1) NW_PCASE(2, 2) NW_PCASE(1, 4)
 #undef NW_PCASE
         default: return (int)hipErrorInvalidValue;
     }

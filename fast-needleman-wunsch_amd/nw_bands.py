@@ -47,8 +47,7 @@ def resident_waves(device: int = 0, substrips: int = 0, strip_waves: int = 0, ke
     import torch
     cus = torch.cuda.get_device_properties(device).multi_processor_count
     if kernel == nwhip.KERNEL_PANELS:
-        c, nw = substrips or 4, strip_waves or 1
-        return cus * max(1, min(LDS_PER_CU // nwhip.panel_lds_bytes(c, nw), 32 // (2 * nw)))
+        return cus  # one panel workgroup per CU (nw_capi.cpp make_shape)
     return cus * (LDS_PER_CU // nwhip.strip_lds_bytes(*nwhip.strip_shape(substrips, strip_waves)))
 
 

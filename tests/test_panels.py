@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 SCHEMES = oracle.SCHEMES
 P = nwhip.KERNEL_PANELS
 # every supported panel shape (C columns per lane, NW compute waves per panel)
-PANEL_SHAPES = [(4, 4), (2, 8), (4, 2), (2, 4), (4, 1), (2, 2), (1, 4), (1, 8)]
+PANEL_SHAPES = [(4, 4), (4, 2), (2, 4), (4, 1), (2, 2), (1, 4)]
 
 
 @pytest.fixture(scope="module")
@@ -100,7 +100,7 @@ def test_panel_worker_count(torch, ctx, waves, panel):
 
 
 @pytest.mark.parametrize("scheme", [(1, -1, -1), (1, 0, -1), (2, -1, -2)])
-@pytest.mark.parametrize("panel", [(4, 4), (2, 4), (4, 1), (1, 4), (2, 8)])
+@pytest.mark.parametrize("panel", [(4, 4), (2, 4), (4, 1), (1, 4), (2, 2)])
 @pytest.mark.parametrize("n1,n2,alpha", [(1, 1, 4), (63, 64, 4), (300, 1000, 4), (1500, 1100, 4),
                                          (1000, 300, 20), (4100, 513, 4)])
 def test_panel_sw_vs_oracle(torch, ctx, scheme, panel, n1, n2, alpha):
