@@ -36,8 +36,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--n", type=int, default=262144, help="sequence length (N x N table)")
-    ap.add_argument("--scheme", default="1,0,-1", help="match,mismatch,gap")
+    ap.add_argument("--n", type=int, default=None,
+                    help="sequence length, N x N table (default: 262144 for nw, 65536 for sw)")
+    ap.add_argument("--scheme", default=None,
+                    help="match,mismatch,gap (default: 1,0,-1 for nw = the reference as shipped; "
+                         "1,-1,-1 for sw)")
     ap.add_argument("--waves", type=int, default=0)
     ap.add_argument("--substrips", type=int, default=0, help="columns per lane C (0 = auto)")
     ap.add_argument("--strip-waves", type=int, default=0,
@@ -61,7 +64,13 @@ def parse():
                     help="nw: the headline NW fill (config 3); sw: Smith-Waterman + traceback (config 5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-n", type=int, default=32768, help="CPU baseline sample side")
-    return ap.parse_args()
+    args = ap.parse_args()
+    # per-workload defaults; values the user passed are never rewritten
+    if args.n is None:
+        args.n = 65536 if args.workload == "sw" else 262144
+    if args.scheme is None:
+        args.scheme = "1,-1,-1" if args.workload == "sw" else "1,0,-1"
+    return args
 
 
 def golden_score(n: int, scheme) -> int | None:
@@ -162,9 +171,9 @@ def run_single(args):
     tab = nwhip.Context.alloc_table(n, n)
     stream = torch.cuda.current_stream()
 
+    kw = dict(waves=args.waves, substrips=args.substrips, strip_waves=args.strip_waves, kernel=args.kernel)
     for _ in range(args.warmup):
-        ctx.fill(s1, s2, tab, scheme, waves=args.waves, sync=False, substrips=args.substrips,
-                 strip_waves=args.strip_waves)
+        ctx.fill(s1, s2, tab, scheme, sync=False, **kw)
     torch.cuda.synchronize()
 
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -173,8 +182,7 @@ def run_single(args):
     t0 = time.perf_counter()
     for e0, e1 in evs:
         e0.record(stream)
-        ctx.fill(s1, s2, tab, scheme, waves=args.waves, sync=False, substrips=args.substrips,
-                 strip_waves=args.strip_waves)
+        ctx.fill(s1, s2, tab, scheme, sync=False, **kw)
         e1.record(stream)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
@@ -182,6 +190,7 @@ def run_single(args):
     if status != 0:
         raise RuntimeError(f"fill reported status {status} ({nwhip.strerror(status)})")
     kms = [e0.elapsed_time(e1) for e0, e1 in evs]
+    shape = ctx.fill(s1, s2, tab, scheme, **kw)  # (one more fill, untimed: what ran)
     score = int(tab[n, n].item())
     want = golden_score(n, scheme)
     cells = n * n
@@ -205,7 +214,9 @@ def run_single(args):
         "data": "synthetic (i.i.d. uniform {1,2,3,4}, seeds 1/2)",
         "config": {"workload": workload, "n1": n, "n2": n, "scheme": list(scheme),
                    "table_bytes": int(table_bytes), "layout": "row-major int32, pitch "
-                   f"{nwhip.table_pitch(n)}", "waves": args.waves or "auto", "parallelism": "single GPU"},
+                   f"{nwhip.table_pitch(n)}", "waves": args.waves or "auto", "parallelism": "single GPU",
+                   "kernel": {1: "strips", 2: "panels"}.get(shape.kernel, "?"),
+                   "shape": [shape.substrips, shape.strip_waves]},
         "score": score,
         "score_golden": want,
         "score_ok": (want == score) if want is not None else None,
@@ -230,8 +241,8 @@ def run_sw(args):
     import hashlib
     import torch
     import nwhip
-    scheme = tuple(int(x) for x in args.scheme.split(",")) if args.scheme != "1,0,-1" else (1, -1, -1)
-    n = args.n if args.n != 262144 else 65536
+    scheme = tuple(int(x) for x in args.scheme.split(","))
+    n = args.n
     torch.cuda.set_device(0)
     ctx = nwhip.Context(0)
     s1 = torch.from_numpy(nwhip.synth(1, n)).cuda()
@@ -240,7 +251,7 @@ def run_sw(args):
 
     def step():
         r = ctx.fill(s1, s2, tab, scheme, substrips=args.substrips, strip_waves=args.strip_waves,
-                     mode=nwhip.MODE_SW)
+                     mode=nwhip.MODE_SW, kernel=args.kernel)
         al, ops = ctx.sw_traceback(s1, s2, tab, (r.end_i, r.end_j), scheme)
         return r, al, ops
 

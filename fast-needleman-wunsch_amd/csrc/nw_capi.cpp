@@ -89,20 +89,31 @@ constexpr int kLdsPerCU = 160 * 1024;
 // stores, and wants the shape with the shortest hop: measured with
 // tools/rect_time.py, 524288 x 8191 fills in 15.5 ms with (4,1) against 19.9
 // (2,2) and 29.7 (1,4); 524288 x 65535 in 33.0 ms with (2,2), 33.7 (4,1), 37.4 (1,4).
-void tuned_shape(int64_t n1, int64_t n2, int32_t *c, int32_t *nc) {
+void tuned_shape(int64_t n1, int64_t n2, int32_t *c, int32_t *nc, int32_t *kernel = nullptr, int cus = 0) {
     const double cells = (double)(n1 + 1) * (double)(n2 + 1);
     *c = 2;
     *nc = 2;
+    if (kernel) *kernel = NW_KERNEL_STRIPS;
     if (n1 + 1 >= 4 * (n2 + 1) && n1 >= 65536) {
         *c = n2 + 1 <= 32768 ? 4 : 2;
         *nc = n2 + 1 <= 32768 ? 1 : 2;
         return;
     }
-    for (const auto &e : nw::kTuned)
-        if (cells >= e.min_cells && nw::shape_ok(e.c, e.nc)) {
-            *c = e.c;
-            *nc = e.nc;
+    // a panel entry applies only when every CU gets a panel in one pass (the
+    // table is measured on squares; a tall narrow table with as many cells would
+    // leave CUs idle) -- otherwise the last strip entry that applies stands
+    for (const auto &e : nw::kTuned) {
+        if (cells < e.min_cells) continue;
+        if (e.kernel == NW_KERNEL_PANELS) {
+            if (!kernel || !nw::panel_shape_ok(e.c, e.nc) || n1 + 1 < (int64_t)cus * nw::kWave * e.c * e.nc) continue;
+            *kernel = NW_KERNEL_PANELS;
+        } else {
+            if (!nw::shape_ok(e.c, e.nc)) continue;
+            if (kernel) *kernel = NW_KERNEL_STRIPS;
         }
+        *c = e.c;
+        *nc = e.nc;
+    }
 }
 
 // col0: first swept column (1 when the table's column 1 starts a 256-byte line)
@@ -127,7 +138,10 @@ Shape make_shape(int64_t n1, int64_t n2, int32_t waves_req, int32_t sub_req, int
                  int cus, int64_t col0, bool sw = false, int32_t kernel_req = NW_KERNEL_AUTO) {
     Shape s;
     s.kernel = kernel_req == NW_KERNEL_PANELS ? NW_KERNEL_PANELS : NW_KERNEL_STRIPS;
-    if (s.kernel == NW_KERNEL_PANELS) {
+    if (kernel_req == NW_KERNEL_AUTO && sub_req <= 0 && nc_req <= 0 && !sw) {
+        // the measured choice of kernel family and shape (csrc/nw_tuned.h)
+        tuned_shape(n1, n2, &s.K, &s.NC, &s.kernel, cus);
+    } else if (s.kernel == NW_KERNEL_PANELS) {
         if (sub_req <= 0 && nc_req <= 0) {
             panel_auto(n1, cus, &s.K, &s.NC);
         } else {
@@ -167,6 +181,10 @@ Shape make_shape(int64_t n1, int64_t n2, int32_t waves_req, int32_t sub_req, int
     s.gstride = s.nblocks * nw::kWave;
     return s;
 }
+
+// Row / column band fills: AUTO means the strips (the tuned table is measured
+// on whole square tables, and a band's geometry is set by its caller).
+int32_t band_kernel(int32_t k) { return k == NW_KERNEL_AUTO ? NW_KERNEL_STRIPS : k; }
 
 bool fits_i8(int32_t x) { return x >= -128 && x <= 127; }
 
@@ -299,7 +317,7 @@ void nw_ctx_destroy(nw_ctx *c) {
 static int colband_layout(int64_t n1, int64_t n2, int32_t nb, int32_t r, const nw_params *p, int cus,
                    int64_t *sf, int64_t *sc, int64_t *start, int64_t *ncols) {
     if (!p || n1 < 1 || n2 < 0 || nb < 1 || r < 0 || r >= nb) return NW_ERR_ARG;
-    const Shape s = make_shape(n1, n2, 0, p->substrips, p->strip_waves, cus, 1, false, p->kernel);
+    const Shape s = make_shape(n1, n2, 0, p->substrips, p->strip_waves, cus, 1, false, band_kernel(p->kernel));
     if (!shape_valid(s) || nb > s.nstrips) return NW_ERR_ARG;
     const int64_t W = (int64_t)nw::kWave * s.K * s.NC;
     const int64_t base = s.nstrips / nb, extra = s.nstrips % nb;
@@ -365,7 +383,8 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
         if (band->halo_out && (p->flags & 1)) return NW_ERR_ARG;  // needs the real last row
     }
     NW_HIP_TRY(hipSetDevice(c->device));
-    Shape s = make_shape(n1, n2, p->waves, p->substrips, p->strip_waves, c->cus, col0, sw, p->kernel);
+    Shape s = make_shape(n1, n2, p->waves, p->substrips, p->strip_waves, c->cus, col0, sw,
+                         band || cb ? band_kernel(p->kernel) : p->kernel);
     if (!shape_valid(s)) return NW_ERR_ARG;
     const bool panels = s.kernel == NW_KERNEL_PANELS;
     if (cb) {  // this launch sweeps its band's strips only
@@ -691,7 +710,11 @@ int nw_sw_traceback(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *d_s
         return NW_ERR_ARG;
     if ((end_j > 0 && !d_s1) || (end_i > 0 && !d_s2) || (ops_cap > 0 && !host_ops) || ops_cap < 0)
         return NW_ERR_ARG;
+    if (!valid_params(p) || p->mode != NW_MODE_SW) return NW_ERR_ARG;
     NW_HIP_TRY(hipSetDevice(c->device));
+    // the table may have been filled on any stream (nw_fill_device_async on a
+    // non-blocking stream has no ordering with the null stream used below)
+    NW_HIP_TRY(hipDeviceSynchronize());
     int st;
     const size_t need = (size_t)std::max<int64_t>(end_i + end_j + 1, 1);
     if ((st = grow((void **)&c->ops, &c->ops_cap, need)) != NW_OK) return st;
@@ -895,6 +918,14 @@ int32_t nw_debug_trace_words(void) { return nw::kTraceWords; }
 void nw_tuned_shape(int64_t n1, int64_t n2, int32_t *substrips, int32_t *strip_waves) {
     int32_t c = 2, nc = 2;
     if (n1 >= 0 && n2 >= 0) tuned_shape(n1, n2, &c, &nc);
+    if (substrips) *substrips = c;
+    if (strip_waves) *strip_waves = nc;
+}
+
+void nw_auto_shape(int64_t n1, int64_t n2, int32_t cus, int32_t *kernel, int32_t *substrips, int32_t *strip_waves) {
+    int32_t k = NW_KERNEL_STRIPS, c = 2, nc = 2;
+    if (n1 >= 0 && n2 >= 0) tuned_shape(n1, n2, &c, &nc, &k, std::max(cus, 1));
+    if (kernel) *kernel = k;
     if (substrips) *substrips = c;
     if (strip_waves) *strip_waves = nc;
 }

@@ -60,6 +60,9 @@ constexpr int kFeedRows = 256;   // feed ring of a panel's first wave (a power o
 constexpr int kG = 4;            // rows per group (one v_perm word): ring / feed checks, counters
 constexpr int kBatch = 8;        // rows per store-wave batch
 constexpr int kEnt = 16;         // rows per rowpack entry (16 row characters)
+constexpr int kCharRows = 2048;  // LDS ring of row characters (a power of two)
+constexpr int kCharFill = 1024;  // rows the feeder-in wave streams in per refill
+constexpr int kPanelWords = 8;   // per-panel control words (reset with the wave counters)
 
 // Store waves per compute wave.  Under full HBM load one 1 KB store holds its
 // wave for ~330 cycles (tools/ubench/panel_store: 4 waves x 1 KB per CU reach
@@ -73,16 +76,18 @@ struct Lay {
     static constexpr int kRowB = 4 * kWave * C;   // bytes per ring row
     static constexpr int kRing = kR * kRowB;
     static constexpr int kFeed = NW * kRing;      // byte offset of the feed ring
-    static constexpr int kCtl = kFeed + kFeedRows * 4;
+    static constexpr int kChars = kFeed + kFeedRows * 4;  // row-character ring (1 byte per row)
+    static constexpr int kCtl = kChars + kCharRows;
     // counters per compute wave w (rows 0 .. v-1 done): [0] written into the
     // ring, [1] (last wave) read by the feeder-out wave, [2] read (left values)
     // by wave w+1, [4 + q] read by its store wave q
     static constexpr int kSPW = spw(NW);
     static constexpr int kCtlWords = 8;
     // panel words: [+0] ticket, [+1] t[0][0], [+2] feed rows in the feed ring
-    // (feeder-in), [+3] feed rows read by wave 0
+    // (feeder-in), [+3] feed rows read by wave 0, [+4] row characters in the
+    // character ring (feeder-in)
     static constexpr int kPanelWord = NW * kCtlWords;
-    static constexpr int kBytes = kCtl + (kPanelWord + 4) * 4;
+    static constexpr int kBytes = kCtl + (kPanelWord + kPanelWords) * 4;
     // NW compute waves, NW * kSPW store waves, the feeder-in and feeder-out waves
     static constexpr int kFeedIn = NW * (1 + kSPW);
     static constexpr int kWaves = kFeedIn + 2;
@@ -90,9 +95,6 @@ struct Lay {
 
 static_assert(Lay<4, 4>::kBytes <= 160 * 1024, "ring must fit a CU's LDS");
 static_assert(Lay<4, 4>::kWaves <= 16 && Lay<4, 2>::kWaves <= 16 && Lay<4, 1>::kWaves <= 16, "1024 threads");
-
-// Constant address space: uniform loads of the row characters become s_load.
-typedef __attribute__((address_space(4))) const uint32_t cu32;
 
 // Inclusive max-scan over the 64 lanes.  update_dpp with INT32_MIN (the max
 // identity) as "old" folds into v_max_i32_dpp; lanes with no source keep x.
@@ -185,6 +187,11 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
     const int32_t xleft0 = j0 >= 1 ? left0 - (int32_t)((j0 - 1) * (int64_t)gap) : kNeg;
     // x[i-1][jl-1] of the next row's column 0 (lane 0: the left neighbour's)
     int32_t cp = __builtin_amdgcn_update_dpp(xleft0, x[C - 1], 0x138 /*wave_shr:1*/, 0xF, 0xF, false);
+    // the finals of the current row (what the ring gets); the short-chain form
+    // keeps the pre-carry prefixes in x
+    int32_t wv[C];
+#pragma unroll
+    for (int k = 0; k < C; ++k) wv[k] = x[k];
 
     // ---- per-lane substitution: PERM tables T_k[m] = s(a_k, char m) - off for the
     // mapped row characters m < 8 (7 = in no column: a mismatch); off = 2 GAP
@@ -192,7 +199,7 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
     const int32_t off = SW ? gap : 2 * gap;
     const int32_t msp = A.match - off, mmp = A.mismatch - off;
     const uint32_t mmb = ((uint32_t)mmp & 255u) * 0x01010101u;
-    uint32_t tlo[C], thi[C], ach[C];
+    uint32_t tlo[C], thi[C], ach[C], mk[C];
     int32_t z[C];  // SW: z_j = -GAP*j, the 0 floor in the u form
 #pragma unroll
     for (int k = 0; k < C; ++k) {
@@ -202,6 +209,7 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
         z[k] = (int32_t)(-(int64_t)gap * c);
         if constexpr (PERM) {
             const uint32_t m = (c >= 1 && c <= A.n1) ? (uint32_t)A.charmap[a] : 0xFFu;
+            mk[k] = m;
             const uint32_t sh = 8u * (m & 3u), keep = ~(255u << sh), put = ((uint32_t)msp & 255u) << sh;
             tlo[k] = m < 4u ? ((mmb & keep) | put) : mmb;
             thi[k] = (m >= 4u && m < 8u) ? ((mmb & keep) | put) : mmb;
@@ -209,6 +217,30 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
             tlo[k] = thi[k] = 0u;
         }
     }
+#ifndef NW_ROWS_CHAIN1
+    // T_k[m] = max over k' <= k of max(s'(a_k', char m), tfloor): the prefix of
+    // the carry's own contributions (see row() below), one v_perm per 4 rows
+    const int32_t tfloor = SW ? gap : 0;
+    uint32_t ttlo[C], tthi[C];
+    {
+        int32_t tp[8];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) tp[m] = INT32_MIN;
+#pragma unroll
+        for (int k = 0; k < C; ++k) {
+            uint32_t lo = 0, hi = 0;
+#pragma unroll
+            for (int m = 0; m < 8; ++m) {
+                const int32_t sv = PERM ? (mk[k] == (uint32_t)m ? msp : mmp) : 0;
+                tp[m] = max(tp[m], max(sv, tfloor));
+                const uint32_t b = ((uint32_t)tp[m] & 255u) << (8 * (m & 3));
+                if (m < 4) lo |= b; else hi |= b;
+            }
+            ttlo[k] = lo;
+            tthi[k] = hi;
+        }
+    }
+#endif
 
     // ---- the left column, rows 0 .. : x[r][j0-1]
     //   wave w > 0: wave w-1's last column, read out of w-1's ring;
@@ -293,19 +325,31 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
         }
     };
 
-    // ---- row characters: rowpack16[x + kQOff] = B[x .. x+15], B[y] = s2[y-1]
-    // (mapped for PERM): entry e's 16 rows are one 16-byte entry, s_load'ed two
-    // entries ahead into wd[e & 3]
-    const cu32 *rq = (const cu32 *)A.rowpack;
+    // ---- row characters B[r] = s2[r-1] (mapped for PERM) come out of the LDS
+    // character ring, which the feeder-in wave streams kCharFill rows at a time
+    // far ahead: the compute waves issue no scalar or vector memory loads, so an
+    // LDS wait never waits behind a load that the HBM traffic has slowed.  Rows
+    // 16e .. 16e+15 are read (one broadcast ds_read_b128) two entries ahead into
+    // wd[e & 3].
+    const int32_t *chars_avail = ctl + L::kPanelWord + 4;
+    typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
     uint32_t wd[4][4];
     auto wload = [&](int32_t e, uint32_t (&o)[4]) {
-        const int64_t x0 = ((int64_t)__builtin_amdgcn_readfirstlane(e) * kEnt + kQOff) * 4;
+        const u32x4v v = *(const u32x4v *)(lds + L::kChars + (((uint32_t)e * kEnt) & (kCharRows - 1)));
 #pragma unroll
-        for (int q = 0; q < 4; ++q) o[q] = rq[x0 + q];
+        for (int q = 0; q < 4; ++q) o[q] = v[q];
+    };
+    // every 64-row trip: the characters up to 96 rows ahead must be in the ring
+    auto chars_ready = [&](int32_t need) {
+        if (__builtin_amdgcn_readfirstlane(ctr_load(chars_avail)) < need)
+            dead |= wait_counter(chars_avail, need, A.ctrl, 18, tmo) == kDead;
+        lds_order();
     };
 
+#ifdef NW_ROWS_CHAIN1
     // ---- one row: x (row r-1) -> x (row r), lv = the left value of row r
-    auto row = [&](uint32_t word, const uint32_t (&pks)[C], int q, int32_t lv) {
+    auto row = [&](uint32_t word, const uint32_t (&pks)[C], const uint32_t (&tks)[C], int q, int32_t lv) {
+        (void)tks;
         int32_t pfx[C];
 #pragma unroll
         for (int k = 0; k < C; ++k) {
@@ -329,13 +373,72 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
         for (int k = 0; k < C - 1; ++k) x[k] = max(pfx[k], carry);
         x[C - 1] = S;
         cp = carry;
+#pragma unroll
+        for (int k = 0; k < C; ++k) wv[k] = x[k];
     };
+
+#else
+    // ---- one row, the short-chain form.  State: P[k] = the previous row's
+    // pre-carry prefixes (P[C-1] including its left value) and cp = its carry
+    // into this lane (the final value of column jl-1); its finals are
+    // max(P[k], cp).  Expanding the recurrence in cp,
+    //   m_k = max(W_{k-1} + s_k, W_k) = max(a_k, cp + t_k),
+    //   a_k = max(P_{k-1} + s_k, P_k),  t_k = max(s_k, 0)   (NW, w form)
+    //   a_k = max(P_{k-1} + s_k, P_k + GAP, z_k), t_k = max(s_k, GAP)   (SW, u form)
+    // so the prefix Q_k = max(A_k, cp + T_k) with A, T the prefixes of a, t (T from
+    // a v_perm table): only "cp + T, max3 with A and the left value, 6 DPP scan
+    // steps, the carry" depend on the previous carry -- 9 dependent operations per
+    // row instead of 13.  (The previous row's finals are max(P, cp) because rows
+    // are non-decreasing along j in the w / u form, row 0 included.)
+    auto row = [&](uint32_t word, const uint32_t (&pks)[C], const uint32_t (&tks)[C], int q, int32_t lv) {
+        int32_t Ak[C];
+#pragma unroll
+        for (int k = 0; k < C; ++k) {
+            int32_t a;
+            if constexpr (!SW) {
+                a = k == 0 ? x[0] : max(x[k - 1] + sub_score<MODE>(pks[k], word, q, ach[k], msp, mmp), x[k]);
+            } else {
+                const int32_t up = max(x[k] + gap, z[k]);
+                a = k == 0 ? up : max(x[k - 1] + sub_score<MODE>(pks[k], word, q, ach[k], msp, mmp), up);
+            }
+            Ak[k] = k == 0 ? a : max(Ak[k - 1], a);
+        }
+        int32_t Tk[C];
+        if constexpr (PERM) {
+#pragma unroll
+            for (int k = 0; k < C; ++k) Tk[k] = (int32_t)(int8_t)(uint8_t)(tks[k] >> (8 * q));
+        } else {
+            const int32_t tfl = SW ? gap : 0;
+#pragma unroll
+            for (int k = 0; k < C; ++k) {
+                const int32_t t = max(sub_score<MODE>(0u, word, q, ach[k], msp, mmp), tfl);
+                Tk[k] = k == 0 ? t : max(Tk[k - 1], t);
+            }
+        }
+        const int32_t tot = max(max(Ak[C - 1], cp + Tk[C - 1]), lv);
+        const int32_t S = wave_scan_max(tot);
+        // exclusive carry: lane l-1's final last column; lane 0: the left value
+        const int32_t carry = __builtin_amdgcn_update_dpp(lv, S, 0x138 /*wave_shr:1*/, 0xF, 0xF, false);
+        int32_t Q[C];
+#pragma unroll
+        for (int k = 0; k < C - 1; ++k) Q[k] = max(Ak[k], cp + Tk[k]);
+#pragma unroll
+        for (int k = 0; k < C - 1; ++k) {
+            x[k] = Q[k];                 // pre-carry prefix (state)
+            wv[k] = max(Q[k], carry);    // final (ring)
+        }
+        x[C - 1] = tot;
+        wv[C - 1] = S;
+        cp = carry;
+    };
+#endif
 
     // ---- main loop: trips of 64 rows = 16 groups of kG = 4 rows (compile-time
     // group index, so every register ring above is indexed statically).  Row 0
     // (the initial x) goes into the ring without being computed.  The left
     // values of a group are loaded one group ahead.
     int32_t lvA[kG], lvB[kG];
+    chars_ready(min(kCharFill, nrow_it));
     wload(0, wd[0]);
     wload(1, wd[1]);
     if (src != SRC_BOUND) ring_feed(kG);
@@ -343,6 +446,7 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
     if (src != SRC_BOUND) fbv = ctr_load(prod_written);
     const uint64_t tstart = __builtin_amdgcn_s_memrealtime();
     for (int trip = 0; trip < ntrips && !dead; ++trip) {
+        chars_ready(min(64 * trip + 96, nrow_it));
         static_for<0, 16>([&](auto gc) {
             constexpr int g = decltype(gc)::value;
             const int32_t r0 = 64 * trip + kG * g;
@@ -352,9 +456,16 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
             // this group's substitution word (before anything else is queued on
             // the LDS/SMEM counters: its s_load landed two entries ago)
             const uint32_t word = wd[(g >> 2) & 3][g & 3];
-            uint32_t pks[C];
+            uint32_t pks[C], tks[C];
 #pragma unroll
-            for (int k = 0; k < C; ++k) pks[k] = PERM ? __builtin_amdgcn_perm(thi[k], tlo[k], word) : 0u;
+            for (int k = 0; k < C; ++k) {
+                pks[k] = PERM ? __builtin_amdgcn_perm(thi[k], tlo[k], word) : 0u;
+#ifndef NW_ROWS_CHAIN1
+                tks[k] = PERM ? __builtin_amdgcn_perm(tthi[k], ttlo[k], word) : 0u;
+#else
+                tks[k] = 0u;
+#endif
+            }
             if constexpr ((g & 3) == 0) wload(r0 / kEnt + 2, wd[((g >> 2) + 2) & 3]);
             // the next group's left values
             const int32_t rn = r0 + kG;
@@ -364,14 +475,14 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
             }
 #pragma unroll
             for (int u = 0; u < kG; ++u) {
-                if (!(g == 0 && u == 0) || trip != 0) row(word, pks, u, lv[u]);
+                if (!(g == 0 && u == 0) || trip != 0) row(word, pks, tks, u, lv[u]);
                 char *dst = lds + rlane + (uint32_t)((r0 + u) & (kR - 1)) * L::kRowB;
                 if constexpr (C == 1) {
-                    *(int32_t *)dst = x[0];
+                    *(int32_t *)dst = wv[0];
                 } else if constexpr (C == 2) {
-                    *(int2 *)dst = make_int2(x[0], x[1]);
+                    *(int2 *)dst = make_int2(wv[0], wv[1]);
                 } else {
-                    *(int4 *)dst = make_int4(x[0], x[1], x[2], x[3]);
+                    *(int4 *)dst = make_int4(wv[0], wv[1], wv[2], wv[3]);
                 }
                 if (u == 1) {
                     // counters for the next group's checks, read mid-group so that
@@ -405,32 +516,71 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
     (void)nrows;
 }
 
-// Feeder-in wave of panel p > 0: polls the previous panel's granules (or a
-// column band's feed) 64 rows per load and appends the leading run whose tags
-// match this launch to the feed ring of compute wave 0, publishing rows
-// available in the panel word [+2].  Bounded: gives up (error word) after the
-// watchdog interval without progress.
+// Feeder-in wave: streams the row characters into the character ring, and for
+// panel p > 0 polls the previous panel's granules (or a column band's feed) 64
+// rows per load, appending the leading run whose tags match this launch to the
+// feed ring of compute wave 0 (rows available: panel word [+2]).  Bounded: gives
+// up (error word) after the watchdog interval without progress.
 template <int C, int NW>
 __device__ __forceinline__ void feeder_in(const FillArgs &A, char *__restrict__ lds, int p, int lane) {
     typedef Lay<C, NW> L;
-    if (p == 0) return;  // panel 0's left column is the boundary
+    typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
     int32_t *ctl = (int32_t *)(lds + L::kCtl);
     int32_t *avail_w = ctl + L::kPanelWord + 2;
     const int32_t *cons = ctl + L::kPanelWord + 3;
+    int32_t *chars_w = ctl + L::kPanelWord + 4;
+    const int32_t *slowest = ctl + (NW - 1) * L::kCtlWords;  // rows written by the last compute wave
     int32_t *feed = (int32_t *)(lds + L::kFeed);
     const bool fed = p == A.strip0 && A.feed_in != nullptr;
+    const bool has_feed = p > 0;  // panel 0's left column is the boundary
     const uint64_t *gin = fed ? A.feed_in : A.gran + (int64_t)((p + A.M - 1) % A.M) * A.gstride;
     const uint32_t tag_in = fed ? A.feed_tag : A.tagbase + (uint32_t)p;
     const int32_t nrow_it = 64 * A.nblocks;
     const uint64_t tmo = A.timeout_ticks;
-    int32_t avail = 0, consv = 0;
+    const u32x4v *rq = (const u32x4v *)A.rowpack;
+    // Row characters: rows [cf, cf + kCharFill) per refill; lane l loads the
+    // 16-row entry of rows cf + 16 l (rowpack16[x + kQOff] = B[x .. x+15]).  A
+    // refill overwrites rows cf - kCharRows .. : the last compute wave must have
+    // passed them.
+    int32_t cf = 0;
+    auto refill = [&](bool wait) -> bool {
+        if (cf >= nrow_it) return false;
+        const int32_t need = cf + kCharFill - kCharRows;
+        int32_t sl = __builtin_amdgcn_readfirstlane(ctr_load(slowest));
+        if (sl < need) {
+            if (!wait) return false;
+            sl = wait_counter(slowest, need, A.ctrl, 19, tmo);
+            if (sl == kDead) return false;
+        }
+        lds_order();
+        const int64_t x = (int64_t)min(cf + kEnt * lane, nrow_it) + kQOff;
+        const u32x4v v = rq[x];
+        *(u32x4v *)(lds + L::kChars + ((uint32_t)(cf + kEnt * lane) & (kCharRows - 1))) = v;
+        lds_order();
+        cf += kCharFill;
+        ctr_store(chars_w, cf);
+        return true;
+    };
+    refill(true);
+    refill(true);
+    int32_t avail = has_feed ? 0 : nrow_it, consv = 0;
     uint64_t t_last = __builtin_amdgcn_s_memrealtime();
     while (avail < nrow_it) {
-        // feed-ring space for rows avail .. avail+63
+        if (refill(false)) t_last = __builtin_amdgcn_s_memrealtime();
+        // feed-ring space for rows avail .. avail+63 (not a blocking wait: wave 0
+        // may itself be waiting for a character refill)
         const int32_t need = avail + kWave - kFeedRows;
         if (consv < need) {
-            consv = wait_counter(cons, need, A.ctrl, 16, tmo);
-            if (consv == kDead) break;
+            consv = __builtin_amdgcn_readfirstlane(ctr_load(cons));
+            if (consv < need) {
+                if (ctrl_load(A.ctrl + 1) != 0u) break;
+                if (__builtin_amdgcn_s_memrealtime() - t_last > tmo) {
+                    give_up(A.ctrl, 3u, 16, cons, need, consv);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
         }
         const int32_t r = avail + lane;
         const uint64_t g = gran_load(gin + min(r, nrow_it - 1));
@@ -451,7 +601,11 @@ __device__ __forceinline__ void feeder_in(const FillArgs &A, char *__restrict__ 
             __builtin_amdgcn_s_sleep(1);
         }
     }
-    ctr_store(avail_w, kDone);
+    if (has_feed) ctr_store(avail_w, kDone);
+    // the rest of the row characters
+    while (refill(true)) {
+    }
+    ctr_store(chars_w, kDone);
 }
 
 // Feeder-out wave: publishes the last compute wave's last column, rows 0 .. as
@@ -635,7 +789,7 @@ __global__ __launch_bounds__((64 * Lay<C, NW>::kWaves)) void nw_fill_panels(Fill
 #endif
     for (;;) {
         if (threadIdx.x == 0) {
-            for (int w = 0; w < L::kPanelWord + 4; ++w) ctl[w] = 0;  // (the panel words too)
+            for (int w = 0; w < L::kPanelWord + kPanelWords; ++w) ctl[w] = 0;  // (the panel words too)
             ctl[L::kPanelWord] = (int32_t)atomicAdd(A.ctrl, 1u);
         }
         __syncthreads();

@@ -1,5 +1,5 @@
-// nw_tuned.h -- strip shape per table size for auto-shaped fills (nw_params
-// substrips = strip_waves = 0).  Written by tools/tune.py from measurements on
+// nw_tuned.h -- kernel family and shape per table size for auto fills (nw_params
+// kernel = substrips = strip_waves = 0).  Written by tools/tune.py from measurements on
 // an MI355X (AMD Radeon Graphics; tools/tune_table.json); entries in increasing
 // min_cells, the last one that applies wins.
 #pragma once
@@ -7,14 +7,15 @@
 namespace nw {
 struct TunedShape {
     double min_cells;  // (n1 + 1) * (n2 + 1) at least
-    int c, nc;         // columns per lane, chained compute waves per strip
+    int kernel;        // 1 = strips (nw_fill.hip), 2 = panels (nw_rows.hip)
+    int c, nc;         // columns per lane, chained compute waves per strip / panel
 };
 constexpr TunedShape kTuned[] = {
-    {0.0, 2, 1},  // best at 4096^2: 46 GCUPS
-    {67129345.0, 2, 2},  // best at 16384^2: 203 GCUPS
-    {536920065.0, 2, 2},  // best at 32768^2: 403 GCUPS
-    {2147581953.0, 4, 1},  // best at 65536^2: 701 GCUPS
-    {8590131201.0, 1, 4},  // best at 131072^2: 1027 GCUPS
-    {34360131585.0, 1, 4},  // best at 262144^2: 1291 GCUPS
+    {0.0, 1, 2, 1},  // best at 4096^2: 46 GCUPS
+    {67129345.0, 1, 2, 2},  // best at 16384^2: 203 GCUPS
+    {536920065.0, 1, 2, 2},  // best at 32768^2: 403 GCUPS
+    {2147581953.0, 1, 4, 1},  // best at 65536^2: 701 GCUPS
+    {8590131201.0, 1, 1, 4},  // best at 131072^2: 1027 GCUPS
+    {34360131585.0, 2, 4, 4},  // best at 262144^2: 1463 GCUPS
 };
 }  // namespace nw

@@ -32,7 +32,7 @@ EXPORTS = ["nw_params_default", "nw_strerror", "nw_version", "nw_fill", "nw_tabl
            "nw_fill_device", "nw_fill_device_async", "nw_ctx_status", "nw_read_bdna", "nw_free",
            "nw_synth_bdna", "nw_band_layout", "nw_halo_bytes", "nw_fill_band_async",
            "nw_ipc_get_handle", "nw_ipc_open_handle", "nw_ipc_close_handle", "nw_halo_alloc",
-           "nw_halo_free", "nw_fill_emb", "nw_sw_align", "nw_sw_traceback", "nw_tuned_shape", "nw_debug_ctrl", "nw_debug_set_trace",
+           "nw_halo_free", "nw_fill_emb", "nw_sw_align", "nw_sw_traceback", "nw_tuned_shape", "nw_auto_shape", "nw_debug_ctrl", "nw_debug_set_trace",
            "nw_debug_trace_words", "nw_colband_layout", "nw_feed_bytes", "nw_feed_alloc",
            "nw_fill_colband_async", "nw_link_alloc", "nw_link_wait_async", "nw_link_signal_async",
            "nw_link_status"]
@@ -160,6 +160,9 @@ def lib() -> ctypes.CDLL:
     L.nw_tuned_shape.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(ctypes.c_int32),
                                  ctypes.POINTER(ctypes.c_int32)]
     L.nw_tuned_shape.restype = None
+    L.nw_auto_shape.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32),
+                                ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]
+    L.nw_auto_shape.restype = None
     _i64p = ctypes.POINTER(ctypes.c_int64)
     L.nw_colband_layout.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
                                     ctypes.POINTER(NwParams), _i64p, _i64p, _i64p, _i64p]
@@ -293,6 +296,14 @@ def tuned_shape(n1: int, n2: int) -> tuple[int, int]:
     c, nc = ctypes.c_int32(), ctypes.c_int32()
     lib().nw_tuned_shape(n1, n2, ctypes.byref(c), ctypes.byref(nc))
     return int(c.value), int(nc.value)
+
+
+def auto_shape(n1: int, n2: int, cus: int = 256) -> tuple[int, int, int]:
+    """(kernel, C, NC) a global fill with kernel = substrips = strip_waves = 0 uses
+    for an n1 x n2 table on a device of `cus` CUs (nw_auto_shape)."""
+    k, c, nc = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+    lib().nw_auto_shape(n1, n2, cus, ctypes.byref(k), ctypes.byref(c), ctypes.byref(nc))
+    return int(k.value), int(c.value), int(nc.value)
 
 
 def strip_shape(substrips: int = 0, strip_waves: int = 0, n1: int = -1, n2: int = -1) -> tuple[int, int]:

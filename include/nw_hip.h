@@ -63,8 +63,10 @@ enum {
  *   PANELS: a wave holds a ROW of 64*C columns, computed as a prefix maximum
  *           (lane-local prefix + a 64-lane DPP max-scan) in the w form; rows
  *           leave through a 32-row ring.  Shapes (C, NW compute waves per
- *           panel): (4,4) (2,8) (4,2) (2,4) (4,1) (2,2) (1,4) (1,8).
- *   AUTO:   the measured choice for the table size (nw_tuned_shape). */
+ *           panel): (4,4) (4,2) (2,4) (4,1) (2,2) (1,4).
+ *   AUTO:   with substrips = strip_waves = 0, the measured family and shape
+ *           for the table size (nw_auto_shape); with an explicit shape, STRIPS.
+ *           Smith-Waterman, row-band and column-band AUTO fills use the strips. */
 enum { NW_KERNEL_AUTO = 0, NW_KERNEL_STRIPS = 1, NW_KERNEL_PANELS = 2 };
 
 /* Runtime replacement for the compile-time constants of
@@ -169,6 +171,13 @@ typedef struct nw_ctx nw_ctx;
  * src/common/block-tuner.cpp:26-34, src/block-tune.sh). */
 void nw_tuned_shape(int64_t n1, int64_t n2, int32_t *substrips, int32_t *strip_waves);
 
+/* Kernel family and shape a global-alignment fill with kernel = substrips =
+ * strip_waves = 0 uses for an n1 x n2 table on a device with `cus` compute units
+ * (hipDeviceProp_t.multiProcessorCount): the same measured table, whose panel
+ * entries apply only when every CU gets a panel (n1 + 1 >= cus * 64 * C * NW). */
+void nw_auto_shape(int64_t n1, int64_t n2, int32_t cus, int32_t *kernel, int32_t *substrips,
+                   int32_t *strip_waves);
+
 /* Row pitch (in int32 elements) the library allocates for nCols = n1+1: a
  * multiple of 64 (256-byte rows) with at least 3 columns of slack after column
  * n1, which the strips need to start at column 1 (nw_table_offset).  Any
@@ -215,9 +224,11 @@ int nw_fill_device(nw_ctx *ctx, const int8_t *d_s1, int64_t n1,
                    const int8_t *d_s2, int64_t n2, const nw_params *p,
                    int32_t *d_t, int64_t pitch, void *stream, nw_result *out);
 
-/* Traceback of a device-resident SW table filled by nw_fill_device (mode SW)
- * from (end_i, end_j) (nw_result.end_i/end_j); ops copied to the host as in
- * nw_sw_align. */
+/* Traceback of a device-resident SW table filled by nw_fill_device /
+ * nw_fill_device_async (mode SW) from (end_i, end_j) (nw_result.end_i/end_j);
+ * ops copied to the host as in nw_sw_align.  Synchronous: it first waits for
+ * all work on the device (the fill may be on any stream).  `p` must be a valid
+ * SW parameter set (mode NW_MODE_SW), else NW_ERR_ARG. */
 int nw_sw_traceback(nw_ctx *ctx, const int8_t *d_s1, int64_t n1, const int8_t *d_s2, int64_t n2,
                     const nw_params *p, const int32_t *d_t, int64_t pitch, int64_t end_i, int64_t end_j,
                     uint8_t *ops, int64_t ops_cap, nw_alignment *out);

@@ -106,12 +106,15 @@ def torch_gpu():
 @pytest.mark.parametrize("n1,n2,P", [(300, 200, 2), (1000, 777, 3), (640, 130, 4), (129, 7, 8),
                                      (64 * 37 + 5, 999, 5)])
 @pytest.mark.parametrize("scheme", [(1, 0, -1), (1, -1, -1), (2, -1, -2)])
-def test_local_bands_vs_oracle(torch_gpu, n1, n2, P, scheme):
+@pytest.mark.parametrize("kernel", [1, 2])
+def test_local_bands_vs_oracle(torch_gpu, n1, n2, P, scheme, kernel):
+    """Both kernel families: strips (1) and row-scan panels (2) take the halo row
+    from halo_in granules and publish their last row into halo_out."""
     torch = torch_gpu
     rng = np.random.default_rng(n1 * 31 + n2 + P)
     s1 = rng.integers(1, 5, n1).astype(np.int8)
     s2 = rng.integers(1, 5, n2).astype(np.int8)
-    lb = nw_bands.LocalBands(n1, n2, P)
+    lb = nw_bands.LocalBands(n1, n2, P, kernel=kernel)
     try:
         score = lb.fill(torch.from_numpy(s1).cuda(), torch.from_numpy(s2).cuda(), scheme)
         full = oracle.fill(s1, s2, scheme)
@@ -162,15 +165,22 @@ def test_local_bands_32k_score(torch_gpu):
 
 
 @pytest.mark.gpu
-def test_two_process_bands_shared_gpu(torch_gpu):
+@pytest.mark.parametrize("kernel", [1, 2])
+def test_two_process_bands_shared_gpu(torch_gpu, kernel):
     """The bench's multi-process path end to end on one GPU: 2 ranks (torch.distributed.run,
-    gloo control plane), IPC-mapped halo buffer, in-kernel halo stores."""
+    gloo control plane), IPC-mapped halo / feed buffers alternating by launch parity,
+    link-word flow control between back-to-back launches, in-kernel halo stores; the
+    row-band leg (`value`) and the column-band leg (`alt_partition`) both against the
+    oracle, for both kernel families."""
     n1, rows = 4096 + 17, 700
+    width, crows = 1500, 1300
     env = dict(os.environ, PYTHONPATH=PKG)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
-           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
-           "--share-gpu", "--partition", "rows", "--band-rows", str(rows), "--band-cols", str(n1)]
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "2",
+           "--share-gpu", "--partition", "rows", "--alt-partition", "cols", "--band-rows", str(rows),
+           "--band-cols", str(n1), "--col-width", str(width), "--col-rows", str(crows),
+           "--kernel", str(kernel), "--no-cpu-baseline"]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-3000:]
     line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1]
@@ -178,3 +188,42 @@ def test_two_process_bands_shared_gpu(torch_gpu):
     n2 = 2 * rows
     want = oracle.score(nwhip.synth(1, n1), nwhip.synth(2, n2))
     assert res["score"] == want and res["n_gpus"] == 2 and res["config"]["n2"] == n2
+    alt = res["alt_partition"]
+    assert alt["score"] == oracle.score(nwhip.synth(1, 2 * width), nwhip.synth(2, crows))
+    assert alt["config"]["n1"] == 2 * width
+
+
+def test_launch_schedule_never_rewrites_an_unread_buffer():
+    """The back-to-back launch schedule of nw_bands._sweep, simulated: launch k uses
+    buffer k % 2; the producer's launch k waits for the consumer's "done with k - 2"
+    signal.  Under every interleaving the simulation explores, a buffer is never
+    rewritten before the consumer launch that reads it has finished."""
+    import itertools
+    rng = np.random.default_rng(0)
+    K = 12
+    for _ in range(200):
+        done_c = 0          # consumer launches finished
+        started_p = 0       # producer launches started
+        written = {}        # buffer -> producer launch that last wrote it
+        read_ok = True
+        for step in itertools.count():
+            if done_c >= K:
+                break
+            # the producer may start launch k+1 if the link word allows it
+            k = started_p + 1
+            can_p = k <= K and (k < 3 or done_c >= k - 2)
+            # the consumer may finish launch done_c+1 once the producer wrote it
+            can_c = done_c + 1 <= started_p
+            if can_p and (not can_c or rng.random() < 0.5):
+                b = k % 2
+                prev = written.get(b)
+                if prev is not None and prev > done_c:  # rewriting a buffer not yet consumed
+                    read_ok = False
+                written[b] = k
+                started_p = k
+            elif can_c:
+                kk = done_c + 1
+                read_ok &= written.get(kk % 2) == kk  # reads exactly launch kk's data
+                done_c = kk
+            assert step < 10 * K
+        assert read_ok

@@ -167,6 +167,30 @@ def test_local_colbands_vs_oracle(torch_gpu, n1, n2, P, shape, scheme):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n1,n2,P", [(2000, 300, 2), (3000, 777, 3), (8191, 130, 4), (1100, 1500, 4)])
+@pytest.mark.parametrize("scheme", [(1, 0, -1), (1, -1, -1)])
+@pytest.mark.parametrize("panel", [(0, 0), (4, 1), (1, 4)])
+def test_local_colbands_panels_vs_oracle(torch_gpu, n1, n2, P, scheme, panel):
+    """Column bands with the row-scan panel kernel: a band's first panel takes the
+    left band's last column from feed_in (its feeder-in wave), the band's last panel
+    publishes into feed_out (its feeder-out wave)."""
+    torch = torch_gpu
+    rng = np.random.default_rng(n1 + 7 * n2 + P)
+    s1 = rng.integers(1, 5, n1).astype(np.int8)
+    s2 = rng.integers(1, 5, n2).astype(np.int8)
+    lb = nw_bands.LocalColBands(n1, n2, P, substrips=panel[0], strip_waves=panel[1], kernel=nwhip.KERNEL_PANELS)
+    try:
+        score = lb.fill(torch.from_numpy(s1).cuda(), torch.from_numpy(s2).cuda(), scheme)
+        full = oracle.fill(s1, s2, scheme)
+        assert score == full[-1, -1]
+        for r, (sf, sc, start, ncols) in enumerate(lb.layout):
+            got = lb.tables[r][:n2 + 1, :ncols].cpu().numpy()
+            np.testing.assert_array_equal(got, full[:, start:start + ncols], err_msg=f"band {r}")
+    finally:
+        lb.close()
+
+
+@pytest.mark.gpu
 def test_local_colbands_repeated_launches(torch_gpu):
     """Tags advance per launch; stale feed granules of earlier launches are never taken."""
     torch = torch_gpu
@@ -239,15 +263,17 @@ def test_colband_refusals(torch_gpu):
 
 
 @pytest.mark.gpu
-def test_two_process_colbands_shared_gpu(torch_gpu):
-    """The bench's column-band path end to end on one GPU: 2 ranks, IPC-mapped feed
-    buffer, in-kernel feed stores."""
+@pytest.mark.parametrize("kernel", [1, 2])
+def test_two_process_colbands_shared_gpu(torch_gpu, kernel):
+    """The bench's column-band path as `value` end to end on one GPU: 2 ranks,
+    IPC-mapped feed buffers by launch parity, in-kernel feed stores."""
     width, n2 = 1500, 1300
     env = dict(os.environ, PYTHONPATH=PKG)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
-           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
-           "--share-gpu", "--partition", "cols", "--col-width", str(width), "--col-rows", str(n2)]
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--share-gpu", "--partition", "cols", "--alt-partition", "none", "--col-width", str(width),
+           "--col-rows", str(n2), "--kernel", str(kernel), "--no-cpu-baseline"]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-3000:]
     line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1]

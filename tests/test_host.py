@@ -143,5 +143,23 @@ def test_tuned_shape_is_supported():
         assert nwhip.strip_shape(0, 0, n, n) == (c, nc)
 
 
+def test_auto_shape_picks_supported_kernels():
+    """nw_auto_shape: the tuner's table picks the kernel family too; a panel entry
+    applies only when every CU gets a panel in one pass, else the strip entry."""
+    for n in [0, 1, 100, 4096, 32768, 65536, 131072, 262144, 524288]:
+        k, c, nc = nwhip.auto_shape(n, n, 256)
+        assert k in (nwhip.KERNEL_STRIPS, nwhip.KERNEL_PANELS), (n, k)
+        if k == nwhip.KERNEL_PANELS:
+            assert nwhip.panel_lds_bytes(c, nc) > 0 and n + 1 >= 256 * 64 * c * nc, (n, c, nc)
+        else:
+            assert nwhip.strip_lds_bytes(c, nc) > 0, (n, c, nc)
+    # a tall table with as many cells as the 256k square but narrow: strips
+    assert nwhip.auto_shape(65535, 1 << 20, 256)[0] == nwhip.KERNEL_STRIPS
+    # the panel rule scales with the device's CUs
+    k, c, nc = nwhip.auto_shape(262144, 262144, 256)
+    if k == nwhip.KERNEL_PANELS:
+        assert nwhip.auto_shape(262144, 262144, 512)[0] == nwhip.KERNEL_STRIPS
+
+
 def test_trace_words_exported():
     assert nwhip.trace_words() >= 16

@@ -3,7 +3,8 @@
 (src/common/block-tuner.cpp:26-34 sweeps tile N x M; src/block-tune.sh:3-42 and
 src/buf-tune.sh:3-43 drive it over sizes).
 
-Here the knob is the strip shape (C columns per lane, NC chained compute waves;
+Here the knobs are the kernel family (nw_params.kernel: anti-diagonal strips or
+row-scan panels) and its shape (C columns per lane, NC chained compute waves;
 nw_params.substrips / strip_waves).  Two steps:
 
   on the GPU box:   python tools/tune.py --measure --out gpurun_out/tune.json
@@ -20,7 +21,9 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SHAPES = [(2, 2), (1, 4), (4, 1), (2, 1), (1, 2), (1, 1)]
+# (kernel, C, NC): 1 = strips (nw_fill.hip), 2 = panels (nw_rows.hip)
+SHAPES = [(1, 2, 2), (1, 1, 4), (1, 4, 1), (1, 2, 1), (1, 1, 2), (1, 1, 1),
+          (2, 4, 4), (2, 2, 4), (2, 4, 2), (2, 4, 1), (2, 2, 2), (2, 1, 4)]
 SIZES = [4096, 16384, 32768, 65536, 131072, 262144]
 HEADER = os.path.join(ROOT, "fast-needleman-wunsch_amd", "csrc", "nw_tuned.h")
 
@@ -38,14 +41,14 @@ def measure(args):
         s2 = torch.from_numpy(nwhip.synth(2, n)).cuda()
         tab = nwhip.Context.alloc_table(n, n)
         want = golden.get(f"{n}:1,0,-1")
-        for c, nc in SHAPES:
-            r = ctx.fill(s1, s2, tab, substrips=c, strip_waves=nc)  # warmup (first touch)
+        for kernel, c, nc in SHAPES:
+            r = ctx.fill(s1, s2, tab, substrips=c, strip_waves=nc, kernel=kernel)  # warmup (first touch)
             ts = []
             for _ in range(args.reps):
-                r = ctx.fill(s1, s2, tab, substrips=c, strip_waves=nc)
+                r = ctx.fill(s1, s2, tab, substrips=c, strip_waves=nc, kernel=kernel)
                 ts.append(r.kernel_ms)
             ok = want is None or r.score == want
-            e = {"n": n, "c": c, "nc": nc, "ms": min(ts), "all_ms": [round(t, 3) for t in ts],
+            e = {"n": n, "kernel": kernel, "c": c, "nc": nc, "ms": min(ts), "all_ms": [round(t, 3) for t in ts],
                  "gcups": n * n / (min(ts) * 1e6), "score_ok": ok}
             print(json.dumps(e), flush=True)
             res.append(e)
@@ -71,17 +74,18 @@ def write(args):
         # the shape measured best at size n applies to tables larger than the
         # previous measured size
         lo = 0.0 if i == 0 else float((sizes[i - 1] + 1) * (n + 1))
-        rows.append((lo, best[n]["c"], best[n]["nc"], n, best[n]["gcups"]))
-    lines = ["// nw_tuned.h -- strip shape per table size for auto-shaped fills (nw_params",
-             "// substrips = strip_waves = 0).  Written by tools/tune.py from measurements on",
+        rows.append((lo, best[n].get("kernel", 1), best[n]["c"], best[n]["nc"], n, best[n]["gcups"]))
+    lines = ["// nw_tuned.h -- kernel family and shape per table size for auto fills (nw_params",
+             "// kernel = substrips = strip_waves = 0).  Written by tools/tune.py from measurements on",
              f"// an MI355X ({data.get('device', '?')}; tools/tune_table.json); entries in increasing",
              "// min_cells, the last one that applies wins.",
              "#pragma once", "", "namespace nw {", "struct TunedShape {",
              "    double min_cells;  // (n1 + 1) * (n2 + 1) at least",
-             "    int c, nc;         // columns per lane, chained compute waves per strip",
+             "    int kernel;        // 1 = strips (nw_fill.hip), 2 = panels (nw_rows.hip)",
+             "    int c, nc;         // columns per lane, chained compute waves per strip / panel",
              "};", "constexpr TunedShape kTuned[] = {"]
-    for lo, c, nc, n, g in rows:
-        lines.append(f"    {{{lo:.1f}, {c}, {nc}}},  // best at {n}^2: {g:.0f} GCUPS")
+    for lo, k, c, nc, n, g in rows:
+        lines.append(f"    {{{lo:.1f}, {k}, {c}, {nc}}},  // best at {n}^2: {g:.0f} GCUPS")
     lines += ["};", "}  // namespace nw", ""]
     with open(HEADER, "w") as f:
         f.write("\n".join(lines))
