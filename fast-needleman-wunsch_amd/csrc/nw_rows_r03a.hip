@@ -60,7 +60,6 @@ constexpr int kFeedRows = 256;   // feed ring of a panel's first wave (a power o
 constexpr int kG = 4;            // rows per group (one v_perm word): ring / feed checks, counters
 constexpr int kBatch = 8;        // rows per store-wave batch
 constexpr int kEnt = 16;         // rows per rowpack entry (16 row characters)
-constexpr int kPanelWords = 8;   // per-panel control words (reset with the wave counters)
 
 // Store waves per compute wave.  Under full HBM load one 1 KB store holds its
 // wave for ~330 cycles (tools/ubench/panel_store: 4 waves x 1 KB per CU reach
@@ -83,7 +82,7 @@ struct Lay {
     // panel words: [+0] ticket, [+1] t[0][0], [+2] feed rows in the feed ring
     // (feeder-in), [+3] feed rows read by wave 0
     static constexpr int kPanelWord = NW * kCtlWords;
-    static constexpr int kBytes = kCtl + (kPanelWord + kPanelWords) * 4;
+    static constexpr int kBytes = kCtl + (kPanelWord + 4) * 4;
     // NW compute waves, NW * kSPW store waves, the feeder-in and feeder-out waves
     static constexpr int kFeedIn = NW * (1 + kSPW);
     static constexpr int kWaves = kFeedIn + 2;
@@ -186,11 +185,6 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
     const int32_t xleft0 = j0 >= 1 ? left0 - (int32_t)((j0 - 1) * (int64_t)gap) : kNeg;
     // x[i-1][jl-1] of the next row's column 0 (lane 0: the left neighbour's)
     int32_t cp = __builtin_amdgcn_update_dpp(xleft0, x[C - 1], 0x138 /*wave_shr:1*/, 0xF, 0xF, false);
-    // the finals of the current row (what the ring gets); the short-chain form
-    // keeps the pre-carry prefixes in x
-    int32_t wv[C];
-#pragma unroll
-    for (int k = 0; k < C; ++k) wv[k] = x[k];
 
     // ---- per-lane substitution: PERM tables T_k[m] = s(a_k, char m) - off for the
     // mapped row characters m < 8 (7 = in no column: a mismatch); off = 2 GAP
@@ -198,7 +192,7 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
     const int32_t off = SW ? gap : 2 * gap;
     const int32_t msp = A.match - off, mmp = A.mismatch - off;
     const uint32_t mmb = ((uint32_t)mmp & 255u) * 0x01010101u;
-    uint32_t tlo[C], thi[C], ach[C], mk[C];
+    uint32_t tlo[C], thi[C], ach[C];
     int32_t z[C];  // SW: z_j = -GAP*j, the 0 floor in the u form
 #pragma unroll
     for (int k = 0; k < C; ++k) {
@@ -208,7 +202,6 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
         z[k] = (int32_t)(-(int64_t)gap * c);
         if constexpr (PERM) {
             const uint32_t m = (c >= 1 && c <= A.n1) ? (uint32_t)A.charmap[a] : 0xFFu;
-            mk[k] = m;
             const uint32_t sh = 8u * (m & 3u), keep = ~(255u << sh), put = ((uint32_t)msp & 255u) << sh;
             tlo[k] = m < 4u ? ((mmb & keep) | put) : mmb;
             thi[k] = (m >= 4u && m < 8u) ? ((mmb & keep) | put) : mmb;
@@ -216,30 +209,6 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
             tlo[k] = thi[k] = 0u;
         }
     }
-#ifndef NW_ROWS_CHAIN1
-    // T_k[m] = max over k' <= k of max(s'(a_k', char m), tfloor): the prefix of
-    // the carry's own contributions (see row() below), one v_perm per 4 rows
-    const int32_t tfloor = SW ? gap : 0;
-    uint32_t ttlo[C], tthi[C];
-    {
-        int32_t tp[8];
-#pragma unroll
-        for (int m = 0; m < 8; ++m) tp[m] = INT32_MIN;
-#pragma unroll
-        for (int k = 0; k < C; ++k) {
-            uint32_t lo = 0, hi = 0;
-#pragma unroll
-            for (int m = 0; m < 8; ++m) {
-                const int32_t sv = PERM ? (mk[k] == (uint32_t)m ? msp : mmp) : 0;
-                tp[m] = max(tp[m], max(sv, tfloor));
-                const uint32_t b = ((uint32_t)tp[m] & 255u) << (8 * (m & 3));
-                if (m < 4) lo |= b; else hi |= b;
-            }
-            ttlo[k] = lo;
-            tthi[k] = hi;
-        }
-    }
-#endif
 
     // ---- the left column, rows 0 .. : x[r][j0-1]
     //   wave w > 0: wave w-1's last column, read out of w-1's ring;
@@ -336,10 +305,7 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
     };
 
     // ---- one row: x (row r-1) -> x (row r), lv = the left value of row r
-#ifdef NW_ROWS_CHAIN1
-    // ---- one row: x (row r-1) -> x (row r), lv = the left value of row r
-    auto row = [&](uint32_t word, const uint32_t (&pks)[C], const uint32_t (&tks)[C], int q, int32_t lv) {
-        (void)tks;
+    auto row = [&](uint32_t word, const uint32_t (&pks)[C], int q, int32_t lv) {
         int32_t pfx[C];
 #pragma unroll
         for (int k = 0; k < C; ++k) {
@@ -363,65 +329,7 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
         for (int k = 0; k < C - 1; ++k) x[k] = max(pfx[k], carry);
         x[C - 1] = S;
         cp = carry;
-#pragma unroll
-        for (int k = 0; k < C; ++k) wv[k] = x[k];
     };
-
-#else
-    // ---- one row, the short-chain form.  State: P[k] = the previous row's
-    // pre-carry prefixes (P[C-1] including its left value) and cp = its carry
-    // into this lane (the final value of column jl-1); its finals are
-    // max(P[k], cp).  Expanding the recurrence in cp,
-    //   m_k = max(W_{k-1} + s_k, W_k) = max(a_k, cp + t_k),
-    //   a_k = max(P_{k-1} + s_k, P_k),  t_k = max(s_k, 0)   (NW, w form)
-    //   a_k = max(P_{k-1} + s_k, P_k + GAP, z_k), t_k = max(s_k, GAP)   (SW, u form)
-    // so the prefix Q_k = max(A_k, cp + T_k) with A, T the prefixes of a, t (T from
-    // a v_perm table): only "cp + T, max3 with A and the left value, 6 DPP scan
-    // steps, the carry" depend on the previous carry -- 9 dependent operations per
-    // row instead of 13.  (The previous row's finals are max(P, cp) because rows
-    // are non-decreasing along j in the w / u form, row 0 included.)
-    auto row = [&](uint32_t word, const uint32_t (&pks)[C], const uint32_t (&tks)[C], int q, int32_t lv) {
-        int32_t Ak[C];
-#pragma unroll
-        for (int k = 0; k < C; ++k) {
-            int32_t a;
-            if constexpr (!SW) {
-                a = k == 0 ? x[0] : max(x[k - 1] + sub_score<MODE>(pks[k], word, q, ach[k], msp, mmp), x[k]);
-            } else {
-                const int32_t up = max(x[k] + gap, z[k]);
-                a = k == 0 ? up : max(x[k - 1] + sub_score<MODE>(pks[k], word, q, ach[k], msp, mmp), up);
-            }
-            Ak[k] = k == 0 ? a : max(Ak[k - 1], a);
-        }
-        int32_t Tk[C];
-        if constexpr (PERM) {
-#pragma unroll
-            for (int k = 0; k < C; ++k) Tk[k] = (int32_t)(int8_t)(uint8_t)(tks[k] >> (8 * q));
-        } else {
-            const int32_t tfl = SW ? gap : 0;
-#pragma unroll
-            for (int k = 0; k < C; ++k) {
-                const int32_t t = max(sub_score<MODE>(0u, word, q, ach[k], msp, mmp), tfl);
-                Tk[k] = k == 0 ? t : max(Tk[k - 1], t);
-            }
-        }
-        const int32_t tot = max(max(Ak[C - 1], cp + Tk[C - 1]), lv);
-        const int32_t S = wave_scan_max(tot);
-        // exclusive carry: lane l-1's final last column; lane 0: the left value
-        const int32_t carry = __builtin_amdgcn_update_dpp(lv, S, 0x138 /*wave_shr:1*/, 0xF, 0xF, false);
-        int32_t Q[C];
-#pragma unroll
-        for (int k = 0; k < C - 1; ++k) Q[k] = max(Ak[k], cp + Tk[k]);
-#pragma unroll
-        for (int k = 0; k < C - 1; ++k) {
-            x[k] = Q[k];                 // pre-carry prefix (state)
-            wv[k] = max(Q[k], carry);    // final (ring)
-        }
-        x[C - 1] = tot;
-        wv[C - 1] = S;
-        cp = carry;
-    };
-#endif
 
     // ---- main loop: trips of 64 rows = 16 groups of kG = 4 rows (compile-time
     // group index, so every register ring above is indexed statically).  Row 0
@@ -444,16 +352,9 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
             // this group's substitution word (before anything else is queued on
             // the LDS/SMEM counters: its s_load landed two entries ago)
             const uint32_t word = wd[(g >> 2) & 3][g & 3];
-            uint32_t pks[C], tks[C];
+            uint32_t pks[C];
 #pragma unroll
-            for (int k = 0; k < C; ++k) {
-                pks[k] = PERM ? __builtin_amdgcn_perm(thi[k], tlo[k], word) : 0u;
-#ifndef NW_ROWS_CHAIN1
-                tks[k] = PERM ? __builtin_amdgcn_perm(tthi[k], ttlo[k], word) : 0u;
-#else
-                tks[k] = 0u;
-#endif
-            }
+            for (int k = 0; k < C; ++k) pks[k] = PERM ? __builtin_amdgcn_perm(thi[k], tlo[k], word) : 0u;
             if constexpr ((g & 3) == 0) wload(r0 / kEnt + 2, wd[((g >> 2) + 2) & 3]);
             // the next group's left values
             const int32_t rn = r0 + kG;
@@ -463,14 +364,14 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
             }
 #pragma unroll
             for (int u = 0; u < kG; ++u) {
-                if (!(g == 0 && u == 0) || trip != 0) row(word, pks, tks, u, lv[u]);
+                if (!(g == 0 && u == 0) || trip != 0) row(word, pks, u, lv[u]);
                 char *dst = lds + rlane + (uint32_t)((r0 + u) & (kR - 1)) * L::kRowB;
                 if constexpr (C == 1) {
-                    *(int32_t *)dst = wv[0];
+                    *(int32_t *)dst = x[0];
                 } else if constexpr (C == 2) {
-                    *(int2 *)dst = make_int2(wv[0], wv[1]);
+                    *(int2 *)dst = make_int2(x[0], x[1]);
                 } else {
-                    *(int4 *)dst = make_int4(wv[0], wv[1], wv[2], wv[3]);
+                    *(int4 *)dst = make_int4(x[0], x[1], x[2], x[3]);
                 }
                 if (u == 1) {
                     // counters for the next group's checks, read mid-group so that
@@ -734,7 +635,7 @@ __global__ __launch_bounds__((64 * Lay<C, NW>::kWaves)) void nw_fill_panels(Fill
 #endif
     for (;;) {
         if (threadIdx.x == 0) {
-            for (int w = 0; w < L::kPanelWord + kPanelWords; ++w) ctl[w] = 0;  // (the panel words too)
+            for (int w = 0; w < L::kPanelWord + 4; ++w) ctl[w] = 0;  // (the panel words too)
             ctl[L::kPanelWord] = (int32_t)atomicAdd(A.ctrl, 1u);
         }
         __syncthreads();

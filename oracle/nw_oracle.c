@@ -134,6 +134,37 @@ int32_t nw_oracle_score(const int8_t *s1, int64_t n1, const int8_t *s2, int64_t 
 }
 
 /*
+ * The same linear-memory sweep, copying selected whole rows out: rows[k]
+ * (ascending, each in 0 .. n2) lands in out[k * (n1 + 1) ...].  Exact-cell
+ * golden vectors for tables too large for host RAM (tests/golden/make_big_rows.py).
+ */
+void nw_oracle_rows(const int8_t *s1, int64_t n1, const int8_t *s2, int64_t n2,
+                    int32_t match, int32_t mismatch, int32_t gap,
+                    const int64_t *rows, int64_t nsel, int32_t *out) {
+    const int64_t nCols = n1 + 1;
+    int32_t *a = (int32_t *)malloc(sizeof(int32_t) * (size_t)nCols);
+    int32_t *b = (int32_t *)malloc(sizeof(int32_t) * (size_t)nCols);
+    if (!a || !b) { free(a); free(b); return; }
+    a[0] = 0;
+    for (int64_t j = 1; j < nCols; ++j) a[j] = (int32_t)((uint32_t)a[j - 1] + (uint32_t)gap);
+    int64_t k = 0;
+    while (k < nsel && rows[k] == 0) memcpy(out + (k++) * nCols, a, sizeof(int32_t) * (size_t)nCols);
+    for (int64_t i = 1; i <= n2 && k < nsel; ++i) {
+        const int8_t c = s2[i - 1];
+        int32_t left = (int32_t)((uint32_t)a[0] + (uint32_t)gap);
+        b[0] = left;
+        for (int64_t j = 1; j < nCols; ++j) {
+            left = ref_cell(a[j - 1], a[j], left, s1[j - 1], c, match, mismatch, gap);
+            b[j] = left;
+        }
+        while (k < nsel && rows[k] == i) memcpy(out + (k++) * nCols, b, sizeof(int32_t) * (size_t)nCols);
+        int32_t *tmp = a; a = b; b = tmp;
+    }
+    free(a);
+    free(b);
+}
+
+/*
  * idxarray-mt restatement (src/idxarray/idxarray-mt.cpp:4-70): rows are dealt
  * cyclically to threads (:43); idx[i] is row i's loop variable j (:44); row i
  * may compute column j once idx[i-1] > j (:50-56).  The reference relies on

@@ -50,6 +50,10 @@ def lib() -> ctypes.CDLL:
                                       ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                       _i32p, _i32p, _u64p, _u64p]
         L.nw_oracle_score.restype = ctypes.c_int32
+        L.nw_oracle_rows.argtypes = [_i8p, ctypes.c_int64, _i8p, ctypes.c_int64, ctypes.c_int32,
+                                     ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64),
+                                     ctypes.c_int64, _i32p]
+        L.nw_oracle_rows.restype = None
         L.nw_oracle_fill_idxarray.argtypes = [_i8p, ctypes.c_int64, _i8p, ctypes.c_int64,
                                               ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                               _i32p, ctypes.c_int]
@@ -133,6 +137,18 @@ def score(s1, s2, scheme=(1, 0, -1), want_rows=False):
     sc = L.nw_oracle_score(_p(a, _i8p), a.size, _p(b, _i8p), b.size, *scheme,
                            _p(lr, _i32p), _p(lc, _i32p), _p(rs, _u64p), _p(rw, _u64p))
     return int(sc), lr, lc, rs, rw
+
+
+def rows(s1, s2, scheme, which) -> np.ndarray:
+    """Whole rows `which` (sorted, unique) of the table, (len(which), n1+1) int32,
+    in O(n1) memory (nw_oracle_rows; the recurrence of serial.cpp:21-33)."""
+    a, b = _seq(s1), _seq(s2)
+    w = np.ascontiguousarray(np.asarray(which, dtype=np.int64))
+    assert np.all(np.diff(w) > 0) and (w.size == 0 or (w[0] >= 0 and w[-1] <= b.size))
+    out = np.empty((w.size, a.size + 1), dtype=np.int32)
+    lib().nw_oracle_rows(_p(a, _i8p), a.size, _p(b, _i8p), b.size, *scheme,
+                         w.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), w.size, _p(out, _i32p))
+    return out
 
 
 def band_layout(n2: int, P: int, r: int):

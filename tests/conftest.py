@@ -64,3 +64,16 @@ def big_rows(n1: int, n2: int, scheme):
             d = z[k]
             out[k] = np.cumsum(d, dtype=d.dtype)
     return out
+
+
+def big_full_rows(n1: int, n2: int, scheme):
+    """Exact whole rows of a full-size synthetic workload (make_big_rows.py
+    FULL_JOBS): (row indices, (k, n1+1) int32 rows), or None without a fixture."""
+    import numpy as np
+    name = {(1, 0, -1): "shipped", (1, -1, -1): "mm1"}[tuple(scheme)]
+    path = os.path.join(GOLDEN, f"big_fullrows_{n1}x{n2}_{name}.npz")
+    if not os.path.exists(path):
+        return None
+    z = np.load(path)
+    t = np.concatenate([z["first"][:, None].astype(np.int32), z["d"].astype(np.int32)], axis=1)
+    return z["rows"], np.cumsum(t, axis=1, dtype=np.int32)

@@ -13,6 +13,12 @@ with s1 = synth(seed 1, n1), s2 = synth(seed 2, n2).  Stored
 delta-encoded (np.diff, wrapping) in tests/golden/big_rows_<n1>x<n2>_<scheme>.npz;
 tests/conftest.py big_rows() decodes them.
 
+Exact cells: for the FULL_JOBS below, ~32 whole rows (nw_oracle_rows) -- rows 1,
+63, 64, 65, 255, 256, n2, the band boundaries of the 8-band split where the
+geometry is config 4's, and seeded random rows -- each stored as its column 0
+plus int8 differences along the row, in big_fullrows_<n1>x<n2>_<scheme>.npz
+(tests/conftest.py big_full_rows() decodes them).
+
   config 3 : 262144 x 262144 (and the 65536 / 131072 steps below it)
   config 4 : 524288 columns x 32767 rows -- the row-band geometry of the 8-GPU
              case (524288 columns, 8 bands of 4096 rows; mpi-horz-driver.cpp:31-32)
@@ -33,6 +39,10 @@ JOBS = [(65536, 65536, (1, 0, -1)), (65536, 65536, (1, -1, -1)),
         (131072, 131072, (1, 0, -1)), (131072, 131072, (1, -1, -1)),
         (262144, 262144, (1, 0, -1)), (262144, 262144, (1, -1, -1)),
         (524288, 32767, (1, 0, -1))]
+
+FULL_JOBS = [(65536, 65536, (1, 0, -1)), (262144, 262144, (1, 0, -1)), (262144, 262144, (1, -1, -1)),
+             (524288, 32767, (1, 0, -1))]
+FULL_ROWS = 32
 
 
 def path(n1, n2, scheme):
@@ -55,11 +65,43 @@ def job(n1, n2, scheme):
     return n1, n2, scheme, sc, time.time() - t0
 
 
+def full_path(n1, n2, scheme):
+    return os.path.join(HERE, f"big_fullrows_{n1}x{n2}_{NAMES[tuple(scheme)]}.npz")
+
+
+def pick_rows(n1, n2):
+    """Rows 1, 63, 64, 65, 255, 256, n2; for config 4's geometry the boundaries of
+    its 8 row bands (oracle band layout); then seeded random rows up to FULL_ROWS."""
+    import oracle
+    want = {r for r in (1, 63, 64, 65, 255, 256, n2) if r <= n2}
+    if n1 == 524288:
+        for b in range(1, 8):
+            _, st = oracle.band_layout(n2, 8, b)
+            want |= {st - 1, st, st + 1}
+    rng = np.random.default_rng(n1 * 1000003 + n2)
+    while len(want) < FULL_ROWS:
+        want.add(int(rng.integers(0, n2 + 1)))
+    return np.array(sorted(want), dtype=np.int64)
+
+
+def full_job(n1, n2, scheme):
+    import oracle
+    t0 = time.time()
+    rows = pick_rows(n1, n2)
+    t = oracle.rows(oracle.synth(1, n1), oracle.synth(2, n2), scheme, rows)
+    d = np.diff(t, axis=1)
+    assert np.abs(d).max() < 128
+    np.savez_compressed(full_path(n1, n2, scheme), rows=rows, first=t[:, 0].copy(), d=d.astype(np.int8))
+    return n1, n2, scheme, rows.size, time.time() - t0
+
+
 def main():
-    todo = [j for j in JOBS if not os.path.exists(path(*j))]
-    with ProcessPoolExecutor(max_workers=min(4, max(1, len(todo)))) as ex:
-        for n1, n2, scheme, sc, dt in ex.map(job, *zip(*todo)) if todo else []:
-            print(n1, n2, scheme, sc, f"{dt:.0f}s", flush=True)
+    todo = [(job, j) for j in JOBS if not os.path.exists(path(*j))]
+    todo += [(full_job, j) for j in FULL_JOBS if not os.path.exists(full_path(*j))]
+    with ProcessPoolExecutor(max_workers=min(5, max(1, len(todo)))) as ex:
+        futs = [ex.submit(f, *j) for f, j in todo]
+        for fu in futs:
+            print(*fu.result()[:4], f"{fu.result()[4]:.0f}s", flush=True)
 
 
 if __name__ == "__main__":

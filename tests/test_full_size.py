@@ -3,7 +3,9 @@ vectors from the pinned oracle (tests/golden/make_big_rows.py; the reference
 itself cannot hold these tables in host RAM -- SURVEY.md 8(c)).
 
 Every row of the device table is compared through its (sum, column-weighted sum)
-checksum; the last row and the last column exactly; the final score against
+checksum; the last row and the last column exactly; ~32 whole rows per table
+(rows 1, 63, 64, 65, 255, 256, n2, band boundaries, seeded random rows;
+make_big_rows.py FULL_JOBS) cell by cell; the final score against
 synth_scores.json.  Recurrence: src/serial/serial.cpp:21-33; band partition:
 src/mpi/mpi-horz-driver.cpp:31-32, mpi-horz.cpp:16-40.
 
@@ -22,7 +24,7 @@ import pytest
 
 import nwhip
 import oracle
-from conftest import GOLDEN, big_rows
+from conftest import GOLDEN, big_full_rows, big_rows
 
 SQUARES = [(65536, (1, 0, -1)), (65536, (1, -1, -1)), (131072, (1, 0, -1)), (131072, (1, -1, -1)),
            (262144, (1, 0, -1)), (262144, (1, -1, -1))]
@@ -52,6 +54,32 @@ def test_golden_band_geometry_consistent():
     g = big_rows(524288, 32767, (1, 0, -1))
     assert g["last_row"].size == 524289 and g["row_sum"].size == 32768
     assert g["score"] == g["last_row"][-1] == g["last_col"][-1]
+
+
+FULL = [(65536, 65536, (1, 0, -1)), (262144, 262144, (1, 0, -1)), (262144, 262144, (1, -1, -1)),
+        (524288, 32767, (1, 0, -1))]
+
+
+@pytest.mark.parametrize("n1,n2,scheme", FULL)
+def test_golden_full_rows_consistent(n1, n2, scheme):
+    """The exact-row fixtures agree with the row-level vectors: each row's
+    checksums, and the last row where it is among them."""
+    rows, t = big_full_rows(n1, n2, scheme)
+    g = big_rows(n1, n2, scheme)
+    assert t.shape == (rows.size, n1 + 1) and rows.size >= 32 and rows[-1] == n2
+    assert {1, 63, 64, 65, 255, 256} <= set(rows.tolist())
+    rs, rw = oracle.row_checksums(t)
+    np.testing.assert_array_equal(rs, g["row_sum"][rows])
+    np.testing.assert_array_equal(rw, g["row_wsum"][rows])
+    np.testing.assert_array_equal(t[-1], g["last_row"])
+    np.testing.assert_array_equal(t[:, n1], g["last_col"][rows])
+
+
+def test_golden_64k_full_rows_match_oracle():
+    """Re-derive the 64k exact rows with the oracle here (a few seconds)."""
+    n, scheme = 65536, (1, 0, -1)
+    rows, t = big_full_rows(n, n, scheme)
+    np.testing.assert_array_equal(oracle.rows(oracle.synth(1, n), oracle.synth(2, n), scheme, rows), t)
 
 
 def test_golden_64k_rows_match_oracle():
@@ -98,7 +126,27 @@ def row_checksums(torch, tab, rows, n_cols, chunk=256, col_first=0, col_base=0):
     return (torch.cat(rs).numpy().view(np.uint64), torch.cat(rw).numpy().view(np.uint64))
 
 
-def check_square(torch, ctx, n, schemes, substrips=0, strip_waves=0):
+def check_full_rows(torch, tab, n1, n2, scheme, row0=0, col_base=0, ncols=None, nrows=None):
+    """Cell-by-cell comparison of the fixture's exact rows that fall in this
+    table (global rows row0 .. row0 + nrows - 1, global columns col_base ..
+    col_base + ncols - 1)."""
+    fr = big_full_rows(n1, n2, scheme)
+    if fr is None:
+        return 0
+    rows, want = fr
+    ncols = n1 + 1 if ncols is None else ncols
+    nrows = n2 + 1 - row0 if nrows is None else nrows
+    sel = [k for k, r in enumerate(rows) if row0 <= r < row0 + nrows]
+    for k in sel:
+        got = tab[int(rows[k]) - row0, :ncols].cpu().numpy()
+        exp = want[k, col_base:col_base + ncols]
+        bad = np.flatnonzero(got != exp)
+        assert bad.size == 0, (f"row {rows[k]}: {bad.size} cells differ, first col "
+                               f"{col_base + bad[0]} got {got[bad[0]]} want {exp[bad[0]]} ({scheme})")
+    return len(sel)
+
+
+def check_square(torch, ctx, n, schemes, substrips=0, strip_waves=0, kernel=0):
     torch.cuda.empty_cache()
     s1 = torch.from_numpy(nwhip.synth(1, n)).cuda()
     s2 = torch.from_numpy(nwhip.synth(2, n)).cuda()
@@ -106,7 +154,7 @@ def check_square(torch, ctx, n, schemes, substrips=0, strip_waves=0):
     try:
         for scheme in schemes:
             g = big_rows(n, n, scheme)
-            r = ctx.fill(s1, s2, tab, scheme, substrips=substrips, strip_waves=strip_waves)
+            r = ctx.fill(s1, s2, tab, scheme, substrips=substrips, strip_waves=strip_waves, kernel=kernel)
             assert r.status == 0
             assert r.score == g["score"]
             np.testing.assert_array_equal(tab[n, :n + 1].cpu().numpy(), g["last_row"])
@@ -114,6 +162,7 @@ def check_square(torch, ctx, n, schemes, substrips=0, strip_waves=0):
             rs, rw = row_checksums(torch, tab, n + 1, n + 1)
             bad = np.flatnonzero((rs != g["row_sum"]) | (rw != g["row_wsum"]))
             assert bad.size == 0, f"{bad.size} rows differ, first {bad[:5].tolist()} ({scheme})"
+            check_full_rows(torch, tab, n, n, scheme)
     finally:
         del tab
         torch.cuda.empty_cache()
@@ -121,9 +170,11 @@ def check_square(torch, ctx, n, schemes, substrips=0, strip_waves=0):
 
 @pytest.mark.gpu
 @pytest.mark.slow
-def test_config3_256k_every_row(torch, ctx):
-    """BASELINE config 3: 262144 x 262144 on one MI355X, both schemes, every row."""
-    check_square(torch, ctx, 262144, [(1, 0, -1), (1, -1, -1)])
+@pytest.mark.parametrize("kernel", [nwhip.KERNEL_AUTO, nwhip.KERNEL_STRIPS])
+def test_config3_256k_every_row(torch, ctx, kernel):
+    """BASELINE config 3: 262144 x 262144 on one MI355X, both schemes, every row,
+    the auto choice (the panels on a 256-CU MI355X) and the strips."""
+    check_square(torch, ctx, 262144, [(1, 0, -1), (1, -1, -1)], kernel=kernel)
 
 
 @pytest.mark.gpu
@@ -162,6 +213,7 @@ def test_config4_band_geometry(torch):
             np.testing.assert_array_equal(rs, g["row_sum"][start:start + rows], err_msg=f"band {r}")
             np.testing.assert_array_equal(rw, g["row_wsum"][start:start + rows], err_msg=f"band {r}")
             np.testing.assert_array_equal(tab[:rows, n1].cpu().numpy(), g["last_col"][start:start + rows])
+            check_full_rows(torch, tab, n1, n2, (1, 0, -1), row0=start, nrows=rows)
         rows, _ = lb.layout[-1]
         np.testing.assert_array_equal(lb.tables[-1][rows - 1, :n1 + 1].cpu().numpy(), g["last_row"])
     finally:
@@ -195,6 +247,7 @@ def test_config4_colband_geometry(torch):
             rw_all += rw
             np.testing.assert_array_equal(tab[n2, :ncols].cpu().numpy(), g["last_row"][start:start + ncols],
                                           err_msg=f"band {r}")
+            assert check_full_rows(torch, tab, n1, n2, (1, 0, -1), col_base=start, ncols=ncols) >= 32
         np.testing.assert_array_equal(rs_all, g["row_sum"])
         np.testing.assert_array_equal(rw_all, g["row_wsum"])
         np.testing.assert_array_equal(lb.tables[-1][:n2 + 1, lb.layout[-1][3] - 1].cpu().numpy(), g["last_col"])

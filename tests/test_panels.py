@@ -126,7 +126,8 @@ def test_panel_sw_vs_oracle(torch, ctx, scheme, panel, n1, n2, alpha):
 @pytest.mark.parametrize("panel", [(0, 0), (4, 1), (2, 2), (1, 4)])
 def test_panel_64k_every_row(torch, ctx, scheme, panel):
     """65536 x 65536: every row's (sum, weighted sum) checksums, the last row and
-    column and the score against the pinned linear-memory oracle's vectors."""
+    column, 32 whole rows (scheme (1, 0, -1)) and the score against the pinned
+    linear-memory oracle's vectors."""
     from test_gpu_parity import device_row_checksums
     n = 65536
     g = big_rows(n, n, scheme)
@@ -140,3 +141,5 @@ def test_panel_64k_every_row(torch, ctx, scheme, panel):
     rs, rw = device_row_checksums(torch, tab, n + 1, n + 1)
     np.testing.assert_array_equal(rs, g["row_sum"])
     np.testing.assert_array_equal(rw, g["row_wsum"])
+    from test_full_size import check_full_rows
+    check_full_rows(torch, tab, n, n, scheme)  # exact cells where the fixture has rows
