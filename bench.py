@@ -133,7 +133,10 @@ def cpu_baseline(n: int, scheme):
                          if kk in v} | ({"error": v["error"]} if "error" in v else {})
                      for k, v in legs.items()},
             "host": _host_cpu(), "physical_cores": phys, "cpu_share": share,
-            "omp_num_threads_env": omp_env}
+            "omp_num_threads_env": omp_env,
+            "all_cores_cap": (f"idxarray_mt_all runs {usable} threads: capped by OMP_NUM_THREADS={omp_env}, "
+                              "the CPU share the GPU box grants one GPU's job" if usable < min(phys, share)
+                              else f"idxarray_mt_all runs all {usable} usable physical cores")}
 
 
 def _host_cpu() -> str:
@@ -147,15 +150,23 @@ def _host_cpu() -> str:
     return "unknown"
 
 
-def pmc_traffic(workload: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/)."""
+def pmc_traffic(workload: str, kernel: str):
+    """HBM bytes per launch of this workload's fill kernel from the committed
+    rocprofv3 PMC summary (profiles/pmc_traffic.json: WRITE_SIZE + 2 x FETCH_SIZE,
+    the gfx950 correction of MI355X_MICROARCH.md), and where it came from.  Not
+    measured in this run: PMC passes are separate rocprofv3 runs
+    (tools/profile_round.sh)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
-        return None
+        return None, None
     with open(path) as f:
         d = json.load(f)
-    e = d.get(workload)
-    return e.get("hbm_bytes_per_launch") if e else None
+    e = d.get(f"{workload}:{kernel}")
+    if not e:
+        return None, None
+    return e.get("hbm_bytes_per_launch"), (f"profiles/pmc_traffic.json [{workload}:{kernel}], "
+                                           f"{e.get('round', '?')} {e.get('date', '')}, "
+                                           f"kernel {e.get('kernel_name', '?')}").strip()
 
 
 def run_single(args):
@@ -199,6 +210,8 @@ def run_single(args):
     table_bytes = 4.0 * (n + 1) * (n + 1)
     achieved = table_bytes / (avg_ms * 1e6)  # GB/s, algorithmic bytes (4 B per cell)
     workload = f"nw_fill_{n}x{n}"
+    kname = {1: "strips", 2: "panels"}.get(shape.kernel, "?")
+    traffic, traffic_src = pmc_traffic(workload, kname)
     out = {
         "metric": "GCUPS (DP cell updates/s) on NxN NW fill, bit-exact score",
         "value": round(value, 2),
@@ -215,14 +228,14 @@ def run_single(args):
         "config": {"workload": workload, "n1": n, "n2": n, "scheme": list(scheme),
                    "table_bytes": int(table_bytes), "layout": "row-major int32, pitch "
                    f"{nwhip.table_pitch(n)}", "waves": args.waves or "auto", "parallelism": "single GPU",
-                   "kernel": {1: "strips", 2: "panels"}.get(shape.kernel, "?"),
+                   "kernel": kname,
                    "shape": [shape.substrips, shape.strip_waves]},
         "score": score,
         "score_golden": want,
         "score_ok": (want == score) if want is not None else None,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                     "traffic": pmc_traffic(workload),
+                     "traffic": traffic, "traffic_source": traffic_src,
                      "kernel_ms_avg": round(avg_ms, 3), "bytes_per_launch": int(table_bytes)},
         "kernel": nwhip.version(),
     }

@@ -212,6 +212,47 @@ def test_local_colbands_repeated_launches(torch_gpu):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kernel", [nwhip.KERNEL_STRIPS, nwhip.KERNEL_PANELS])
+def test_colband_then_whole_fill_on_one_context(torch_gpu, kernel):
+    """A column band r > 0 (global strips strip0 .. of the table's sweep, tags
+    tagbase + p + 1 with p the GLOBAL strip) followed by whole-table fills on the
+    SAME context: the whole fill must never take a granule the band left behind
+    (tagbase moves past strip0 + nstrips; nw_capi.cpp launch_fill)."""
+    torch = torch_gpu
+    n1, n2, P = 6000, 700, 3
+    rng = np.random.default_rng(77)
+    s1 = rng.integers(1, 5, n1).astype(np.int8)
+    s2 = rng.integers(1, 5, n2).astype(np.int8)
+    d1, d2 = torch.from_numpy(s1).cuda(), torch.from_numpy(s2).cuda()
+    full = oracle.fill(s1, s2)
+    sh = (1, 1) if kernel == nwhip.KERNEL_STRIPS else (4, 1)
+    lay = [nwhip.colband_layout(n1, n2, P, r, sh[0], sh[1], kernel=kernel) for r in range(P)]
+    ctx, ctx0 = nwhip.Context(0), nwhip.Context(0)
+    feeds = [nwhip.Feed(n2, 0) for _ in range(P - 1)]
+    try:
+        for it in range(2):
+            tabs = [nwhip.Context.alloc_table(ncols - 1, n2) for (_, _, _, ncols) in lay]
+            # band 0 on its own context, bands 1 .. on the shared one, in order
+            for r in range(P):
+                (ctx0 if r == 0 else ctx).fill_colband(
+                    d1, d2, tabs[r], P, r, feed_in=feeds[r - 1].ptr if r else None,
+                    feed_out=feeds[r].ptr if r + 1 < P else None, tag=it + 1,
+                    substrips=sh[0], strip_waves=sh[1], kernel=kernel)
+                torch.cuda.synchronize()
+            for r, (_, _, st, ncols) in enumerate(lay):
+                np.testing.assert_array_equal(tabs[r][:n2 + 1, :ncols].cpu().numpy(), full[:, st:st + ncols])
+            tab = nwhip.Context.alloc_table(n1, n2)
+            res = ctx.fill(d1, d2, tab, substrips=sh[0], strip_waves=sh[1], kernel=kernel)
+            assert res.status == 0
+            np.testing.assert_array_equal(tab[:n2 + 1, :n1 + 1].cpu().numpy(), full, err_msg=f"iteration {it}")
+    finally:
+        for f in feeds:
+            f.free()
+        ctx.close()
+        ctx0.close()
+
+
+@pytest.mark.gpu
 def test_local_colbands_32k_score(torch_gpu):
     """BASELINE config-2 inputs split into 4 concurrent column bands on one GPU."""
     torch = torch_gpu

@@ -9,7 +9,7 @@ for d in sys.argv[1:]:
     nd = collections.defaultdict(set)
     for f in sorted(glob.glob(f"{d}/pmc*/pmc_counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            if "fill_strips" not in r["Kernel_Name"]:
+            if "nw_fill_" not in r["Kernel_Name"]:
                 continue
             tot[r["Counter_Name"]] += float(r["Counter_Value"])
             nd[r["Counter_Name"]].add(r["Dispatch_Id"])

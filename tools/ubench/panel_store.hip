@@ -51,18 +51,35 @@ static void run(char *t, long pitchb, long nrows, int lag) {
 }
 
 int main(int argc, char **argv) {
-    const long n = 262144, pitch = 262208, nrows = n + 1;
+    // panel_store [pitch slack in int32, default 64] [lags, default 0,9,64,256] [all shapes 0/1]
+    const long n = 262144, nrows = n + 1;
+    const long slack = argc > 1 ? atol(argv[1]) : 64;
+    const long pitch = n + slack;
     const long pitchb = pitch * 4;
+    const bool all = argc > 3 ? atoi(argv[3]) != 0 : true;
     char *t = nullptr;
     if (hipMalloc(&t, (size_t)(nrows * pitchb + 4096)) != hipSuccess) {
         printf("alloc failed\n");
         return 1;
     }
-    for (int lag : {0, 9, 64, 256}) {
-        run<4, 1>(t, pitchb, nrows, lag);
-        run<4, 8>(t, pitchb, nrows, lag);
+    printf("pitch %ld (slack %ld)\n", pitch, slack);
+    int lags[16], nl = 0;
+    if (argc > 2) {
+        for (char *q = argv[2]; *q && nl < 16;) {
+            lags[nl++] = (int)strtol(q, &q, 10);
+            if (*q == ',') ++q;
+        }
+    } else {
+        lags[0] = 0, lags[1] = 9, lags[2] = 64, lags[3] = 256, nl = 4;
+    }
+    for (int li = 0; li < nl; ++li) {
+        const int lag = lags[li];
+        if (all) {
+            run<4, 1>(t, pitchb, nrows, lag);
+            run<4, 8>(t, pitchb, nrows, lag);
+            run<12, 8>(t, pitchb, nrows, lag);
+        }
         run<8, 8>(t, pitchb, nrows, lag);
-        run<12, 8>(t, pitchb, nrows, lag);
     }
     (void)hipFree(t);
     return 0;
