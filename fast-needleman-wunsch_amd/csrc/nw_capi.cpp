@@ -9,10 +9,13 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <thread>
+#include <vector>
 
 #include "nw_hip.h"
 #include "nw_internal.h"
@@ -753,37 +756,200 @@ int nw_sw_traceback(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *d_s
     return NW_OK;
 }
 
+// ---- host-buffer entry points (the drop-in path) ----------------------------
+//
+// One HostPath per device, created on first use and kept: the context, the
+// device table and sequence buffers (grow-only: a caller looping over pairs pays
+// no hipMalloc / hipFree of the table per call), a non-blocking copy stream and
+// two pinned staging chunks.  The table comes back to the caller's (pageable)
+// buffer through the staging chunks: DMA of chunk k+1 overlaps the threaded
+// memcpy of chunk k into the caller's rows (tools/d2h_bench.cpp measured the
+// alternatives; DESIGN.md "drop-in path").  nw_host_release frees it all.
+namespace {
+
+struct HostPath {
+    std::mutex mu;
+    nw_ctx *c = nullptr;
+    int32_t *tab = nullptr;  // 256-byte aligned allocation; the table starts nw_table_offset() in
+    size_t tab_cap = 0;
+    int8_t *s1 = nullptr, *s2 = nullptr;
+    size_t s1_cap = 0, s2_cap = 0;
+    char *stage[3] = {nullptr, nullptr, nullptr};
+    hipStream_t copy = nullptr;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+};
+constexpr int kStages = 3;
+
+constexpr size_t kStageBytes = 128u << 20;  // per staging chunk
+// tables up to this size stay cached between calls; a larger one is released
+// when its call returns (it would crowd out the caller's own device work)
+constexpr size_t kKeepTableBytes = 16ull << 30;
+HostPath g_host[64];
+
+void host_trim(HostPath &h) {
+    if (h.tab && h.tab_cap > kKeepTableBytes) {
+        (void)hipFree(h.tab);
+        h.tab = nullptr;
+        h.tab_cap = 0;
+    }
+}
+
+void host_free(HostPath &h) {
+    if (h.c) (void)hipSetDevice(h.c->device);
+    if (h.tab) (void)hipFree(h.tab);
+    if (h.s1) (void)hipFree(h.s1);
+    if (h.s2) (void)hipFree(h.s2);
+    for (int k = 0; k < kStages; ++k) {
+        if (h.stage[k]) (void)hipHostFree(h.stage[k]);
+        if (h.ev[k]) (void)hipEventDestroy(h.ev[k]);
+        h.stage[k] = nullptr;
+        h.ev[k] = nullptr;
+    }
+    if (h.copy) (void)hipStreamDestroy(h.copy);
+    nw_ctx_destroy(h.c);
+    h.c = nullptr;
+    h.tab = nullptr;
+    h.s1 = h.s2 = nullptr;
+    h.tab_cap = h.s1_cap = h.s2_cap = 0;
+    h.copy = nullptr;
+}
+
+// Device and sequence buffers for an n1 x n2 table; copies s1 / s2 in.
+int host_prepare(HostPath &h, int dev, const int8_t *s1, int64_t n1, const int8_t *s2, int64_t n2,
+                 int32_t **d_t, int64_t *pitch) {
+    int st;
+    if (!h.c && (st = nw_ctx_create(dev, &h.c)) != NW_OK) return st;
+    NW_HIP_TRY(hipSetDevice(dev));
+    *pitch = nw_table_pitch(n1);
+    // column 1 on a 256-byte line: the allocation (256-byte aligned) + nw_table_offset
+    const size_t need = (size_t)nw_table_bytes(n1, n2) + 256;
+    if (need > h.tab_cap) {  // (grow drops the old buffer first: one table at a time)
+        if ((st = grow((void **)&h.tab, &h.tab_cap, need)) != NW_OK) return st;
+    }
+    if ((st = grow((void **)&h.s1, &h.s1_cap, (size_t)std::max<int64_t>(n1, 1))) != NW_OK) return st;
+    if ((st = grow((void **)&h.s2, &h.s2_cap, (size_t)std::max<int64_t>(n2, 1))) != NW_OK) return st;
+    if (n1 > 0) NW_HIP_TRY(hipMemcpy(h.s1, s1, (size_t)n1, hipMemcpyHostToDevice));
+    if (n2 > 0) NW_HIP_TRY(hipMemcpy(h.s2, s2, (size_t)n2, hipMemcpyHostToDevice));
+    *d_t = h.tab + (n1 >= 1 ? nw_table_offset() : 0);  // (no column 1 when n1 = 0)
+    return NW_OK;
+}
+
+void par_memcpy(char *dst, const char *src, size_t bytes, int threads) {
+    if (threads <= 1 || bytes < (8u << 20)) {
+        std::memcpy(dst, src, bytes);
+        return;
+    }
+    std::vector<std::thread> ts;
+    const size_t per = (bytes / (size_t)threads + 4095) & ~(size_t)4095;
+    for (int t = 1; t < threads; ++t) {
+        const size_t o = (size_t)t * per;
+        if (o >= bytes) break;
+        ts.emplace_back([=] { std::memcpy(dst + o, src + o, std::min(per, bytes - o)); });
+    }
+    std::memcpy(dst, src, std::min(per, bytes));
+    for (auto &t : ts) t.join();
+}
+
+int copy_threads() {
+    if (const char *e = std::getenv("NW_COPY_THREADS")) return std::max(1, std::atoi(e));
+    return (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
+}
+
+// Rows 0..n2 (n1 + 1 int32 each) of the device table into host rows of
+// `stride` int32 (the reference layout: stride = n1 + 1), through the pinned
+// staging chunks.
+int host_staging(HostPath &h) {
+    for (int k = 0; k < kStages; ++k) {
+        if (!h.stage[k]) NW_HIP_TRY(hipHostMalloc((void **)&h.stage[k], kStageBytes, 0));
+        if (!h.ev[k]) NW_HIP_TRY(hipEventCreateWithFlags(&h.ev[k], hipEventDisableTiming));
+    }
+    if (!h.copy) NW_HIP_TRY(hipStreamCreateWithFlags(&h.copy, hipStreamNonBlocking));
+    return NW_OK;
+}
+
+int host_copy_back(HostPath &h, const int32_t *d_t, int64_t pitch, int64_t n1, int64_t n2, int32_t *host,
+                   int64_t stride) {
+    int st;
+    if ((st = host_staging(h)) != NW_OK) return st;
+    const size_t w = (size_t)(n1 + 1) * 4;
+    const int64_t rows = n2 + 1;
+    const int64_t rpc = std::max<int64_t>(1, (int64_t)(kStageBytes / w));
+    if ((size_t)rpc * w > kStageBytes) {  // one row wider than a chunk: direct
+        NW_HIP_TRY(hipMemcpy2D(host, (size_t)stride * 4, d_t, (size_t)pitch * 4, w, (size_t)rows,
+                               hipMemcpyDeviceToHost));
+        return NW_OK;
+    }
+    const int64_t nch = (rows + rpc - 1) / rpc;
+    const int threads = copy_threads();
+    auto issue = [&](int64_t ch) -> hipError_t {
+        const int64_t r0 = ch * rpc, nr = std::min(rpc, rows - r0);
+        hipError_t e = hipMemcpy2DAsync(h.stage[ch % kStages], w, d_t + r0 * pitch, (size_t)pitch * 4, w,
+                                        (size_t)nr, hipMemcpyDeviceToHost, h.copy);
+        return e == hipSuccess ? hipEventRecord(h.ev[ch % kStages], h.copy) : e;
+    };
+    // the fill ran on the null stream (synchronous), so the copy stream sees the table
+    for (int64_t ch = 0; ch < std::min<int64_t>(kStages, nch); ++ch) NW_HIP_TRY(issue(ch));
+    for (int64_t ch = 0; ch < nch; ++ch) {
+        NW_HIP_TRY(hipEventSynchronize(h.ev[ch % kStages]));
+        const int64_t r0 = ch * rpc, nr = std::min(rpc, rows - r0);
+        const char *src = h.stage[ch % kStages];
+        if (stride * 4 == (int64_t)w) {
+            par_memcpy((char *)(host + r0 * stride), src, (size_t)nr * w, threads);
+        } else {
+            for (int64_t r = 0; r < nr; ++r) std::memcpy(host + (r0 + r) * stride, src + (size_t)r * w, w);
+        }
+        if (ch + kStages < nch) NW_HIP_TRY(issue(ch + kStages));
+    }
+    return NW_OK;
+}
+
+int host_device(const nw_params *p, int *dev) {
+    *dev = p->device;
+    if (*dev < 0 && hipGetDevice(dev) != hipSuccess) return NW_ERR_NODEVICE;
+    if (*dev < 0 || *dev >= 64) return NW_ERR_ARG;
+    return NW_OK;
+}
+
+}  // namespace
+
+int nw_host_warmup(int device) {
+    int dev = device;
+    if (dev < 0 && hipGetDevice(&dev) != hipSuccess) return NW_ERR_NODEVICE;
+    if (dev < 0 || dev >= 64) return NW_ERR_ARG;
+    HostPath &h = g_host[dev];
+    std::lock_guard<std::mutex> lock(h.mu);
+    int st;
+    if (!h.c && (st = nw_ctx_create(dev, &h.c)) != NW_OK) return st;
+    NW_HIP_TRY(hipSetDevice(dev));
+    return host_staging(h);
+}
+
+void nw_host_release(int device) {
+    for (int d = 0; d < 64; ++d) {
+        if (device >= 0 && d != device) continue;
+        std::lock_guard<std::mutex> lock(g_host[d].mu);
+        host_free(g_host[d]);
+    }
+}
+
 int nw_sw_align(const int8_t *s1, int64_t n1, const int8_t *s2, int64_t n2, const nw_params *p,
                 uint8_t *host_ops, int64_t ops_cap, nw_alignment *out) {
     if (!p || p->mode != NW_MODE_SW || !out || n1 < 0 || n2 < 0 || (n1 > 0 && !s1) || (n2 > 0 && !s2))
         return NW_ERR_ARG;
-    int dev = p->device;
-    if (dev < 0 && hipGetDevice(&dev) != hipSuccess) return NW_ERR_NODEVICE;
-    nw_ctx *c = nullptr;
-    int st = nw_ctx_create(dev, &c);
-    if (st != NW_OK) return st;
-    const int64_t pitch = nw_table_pitch(n1);
-    int32_t *d_alloc = nullptr;
-    int8_t *d_s1 = nullptr, *d_s2 = nullptr;
-    if (hipMalloc(&d_alloc, (size_t)nw_table_bytes(n1, n2) + 256) != hipSuccess ||
-        hipMalloc(&d_s1, (size_t)std::max<int64_t>(n1, 1)) != hipSuccess ||
-        hipMalloc(&d_s2, (size_t)std::max<int64_t>(n2, 1)) != hipSuccess)
-        st = NW_ERR_OOM;
-    int32_t *d_t = d_alloc ? d_alloc + (n1 >= 1 ? nw_table_offset() : 0) : nullptr;
-    if (st == NW_OK && n1 > 0 && hipMemcpy(d_s1, s1, (size_t)n1, hipMemcpyHostToDevice) != hipSuccess)
-        st = NW_ERR_HIP;
-    if (st == NW_OK && n2 > 0 && hipMemcpy(d_s2, s2, (size_t)n2, hipMemcpyHostToDevice) != hipSuccess)
-        st = NW_ERR_HIP;
+    int dev, st;
+    if ((st = host_device(p, &dev)) != NW_OK) return st;
+    HostPath &h = g_host[dev];
+    std::lock_guard<std::mutex> lock(h.mu);
+    int32_t *d_t = nullptr;
+    int64_t pitch = 0;
     nw_result r;
     std::memset(&r, 0, sizeof r);
-    if (st == NW_OK) st = nw_fill_device(c, d_s1, n1, d_s2, n2, p, d_t, pitch, nullptr, &r);
-    if (st == NW_OK) st = nw_sw_traceback(c, d_s1, n1, d_s2, n2, p, d_t, pitch, r.end_i, r.end_j, host_ops,
+    st = host_prepare(h, dev, s1, n1, s2, n2, &d_t, &pitch);
+    if (st == NW_OK) st = nw_fill_device(h.c, h.s1, n1, h.s2, n2, p, d_t, pitch, nullptr, &r);
+    if (st == NW_OK) st = nw_sw_traceback(h.c, h.s1, n1, h.s2, n2, p, d_t, pitch, r.end_i, r.end_j, host_ops,
                                           ops_cap, out);
     if (st == NW_OK) out->fill_ms = r.kernel_ms;
-    if (d_alloc) (void)hipFree(d_alloc);
-    if (d_s1) (void)hipFree(d_s1);
-    if (d_s2) (void)hipFree(d_s2);
-    nw_ctx_destroy(c);
+    host_trim(h);
     out->status = st;
     return st;
 }
@@ -796,48 +962,28 @@ int nw_fill(const int8_t *s1, int64_t n1, const int8_t *s2, int64_t n2, const nw
         p = &def;
     }
     if (n1 < 0 || n2 < 0 || (n1 > 0 && !s1) || (n2 > 0 && !s2)) return NW_ERR_ARG;
-    // one context per device per process, created on first use
-    static std::mutex mu;
-    static nw_ctx *ctxs[64] = {nullptr};
-    int dev = p->device;
-    if (dev < 0 && hipGetDevice(&dev) != hipSuccess) return NW_ERR_NODEVICE;
-    if (dev < 0 || dev >= 64) return NW_ERR_ARG;
-    std::lock_guard<std::mutex> lock(mu);
-    if (!ctxs[dev]) {
-        int st = nw_ctx_create(dev, &ctxs[dev]);
-        if (st != NW_OK) return st;
-    }
-    nw_ctx *c = ctxs[dev];
-    NW_HIP_TRY(hipSetDevice(dev));
-    const int64_t pitch = nw_table_pitch(n1);
-    int8_t *d_s1 = nullptr, *d_s2 = nullptr;
+    int dev, st;
+    if ((st = host_device(p, &dev)) != NW_OK) return st;
+    HostPath &h = g_host[dev];
+    std::lock_guard<std::mutex> lock(h.mu);
     int32_t *d_t = nullptr;
+    int64_t pitch = 0;
     nw_result r;
     std::memset(&r, 0, sizeof r);
-    int st = NW_OK;
-    // column 1 on a 256-byte line: the allocation (256-byte aligned) + nw_table_offset
-    int32_t *d_alloc = nullptr;
-    hipError_t e = hipMalloc(&d_alloc, (size_t)nw_table_bytes(n1, n2) + 256);
-    if (e != hipSuccess) return e == hipErrorOutOfMemory ? NW_ERR_OOM : NW_ERR_HIP;
-    d_t = d_alloc + (n1 >= 1 ? nw_table_offset() : 0);  // (no column 1 when n1 = 0)
-    if (hipMalloc(&d_s1, (size_t)std::max<int64_t>(n1, 1)) != hipSuccess ||
-        hipMalloc(&d_s2, (size_t)std::max<int64_t>(n2, 1)) != hipSuccess) {
-        st = NW_ERR_OOM;
+    const auto t0 = std::chrono::steady_clock::now();
+    st = host_prepare(h, dev, s1, n1, s2, n2, &d_t, &pitch);
+    const auto t1 = std::chrono::steady_clock::now();
+    if (st == NW_OK) st = nw_fill_device(h.c, h.s1, n1, h.s2, n2, p, d_t, pitch, nullptr, &r);
+    const auto t2 = std::chrono::steady_clock::now();
+    if (st == NW_OK && host_t) st = host_copy_back(h, d_t, pitch, n1, n2, host_t, n1 + 1);
+    const auto t3 = std::chrono::steady_clock::now();
+    if (std::getenv("NW_HOST_TIMING")) {
+        auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        std::fprintf(stderr, "nw_fill: prepare (context, buffers, H2D) %.1f ms, fill %.1f ms (kernel %.1f), "
+                     "copy back %.1f ms (%.1f GB/s)\n", ms(t0, t1), ms(t1, t2), r.kernel_ms, ms(t2, t3),
+                     host_t ? (double)(n1 + 1) * (n2 + 1) * 4 / (ms(t2, t3) * 1e6) : 0.0);
     }
-    if (st == NW_OK && n1 > 0 && hipMemcpy(d_s1, s1, (size_t)n1, hipMemcpyHostToDevice) != hipSuccess)
-        st = NW_ERR_HIP;
-    if (st == NW_OK && n2 > 0 && hipMemcpy(d_s2, s2, (size_t)n2, hipMemcpyHostToDevice) != hipSuccess)
-        st = NW_ERR_HIP;
-    if (st == NW_OK) st = nw_fill_device(c, d_s1, n1, d_s2, n2, p, d_t, pitch, nullptr, &r);
-    if (st == NW_OK && host_t) {
-        const size_t w = (size_t)(n1 + 1) * sizeof(int32_t);
-        if (hipMemcpy2D(host_t, w, d_t, (size_t)pitch * 4, w, (size_t)(n2 + 1),
-                        hipMemcpyDeviceToHost) != hipSuccess)
-            st = NW_ERR_HIP;
-    }
-    (void)hipFree(d_alloc);
-    if (d_s1) (void)hipFree(d_s1);
-    if (d_s2) (void)hipFree(d_s2);
+    host_trim(h);
     r.status = st;
     if (out) *out = r;
     return st;
@@ -856,40 +1002,20 @@ int nw_fill_emb(const int8_t *s1, int64_t n1, const int8_t *s2, int64_t n2, cons
         p = &def;
     }
     if (!host_t || n1 < 0 || n2 < 0 || (n1 > 0 && !s1) || (n2 > 0 && !s2)) return NW_ERR_ARG;
+    int dev, st;
+    if ((st = host_device(p, &dev)) != NW_OK) return st;
+    HostPath &h = g_host[dev];
+    std::lock_guard<std::mutex> lock(h.mu);
+    int32_t *d_t = nullptr;
+    int64_t pitch = 0;
     nw_result r;
     std::memset(&r, 0, sizeof r);
-    int st = NW_OK;
-    {
-        // nw_fill with the table landing in columns 1 .. n1+1 of rows of n1+2
-        int dev = p->device;
-        if (dev < 0 && hipGetDevice(&dev) != hipSuccess) return NW_ERR_NODEVICE;
-        nw_ctx *c = nullptr;
-        if ((st = nw_ctx_create(dev, &c)) != NW_OK) return st;
-        const int64_t pitch = nw_table_pitch(n1);
-        int32_t *d_alloc = nullptr;
-        int8_t *d_s1 = nullptr, *d_s2 = nullptr;
-        if (hipMalloc(&d_alloc, (size_t)nw_table_bytes(n1, n2) + 256) != hipSuccess ||
-            hipMalloc(&d_s1, (size_t)std::max<int64_t>(n1, 1)) != hipSuccess ||
-            hipMalloc(&d_s2, (size_t)std::max<int64_t>(n2, 1)) != hipSuccess)
-            st = NW_ERR_OOM;
-        int32_t *d_t = d_alloc ? d_alloc + (n1 >= 1 ? nw_table_offset() : 0) : nullptr;
-        if (st == NW_OK && n1 > 0 && hipMemcpy(d_s1, s1, (size_t)n1, hipMemcpyHostToDevice) != hipSuccess)
-            st = NW_ERR_HIP;
-        if (st == NW_OK && n2 > 0 && hipMemcpy(d_s2, s2, (size_t)n2, hipMemcpyHostToDevice) != hipSuccess)
-            st = NW_ERR_HIP;
-        if (st == NW_OK) st = nw_fill_device(c, d_s1, n1, d_s2, n2, p, d_t, pitch, nullptr, &r);
-        const size_t w = (size_t)(n1 + 1) * sizeof(int32_t);
-        if (st == NW_OK && hipMemcpy2D(host_t + 1, (size_t)(n1 + 2) * sizeof(int32_t), d_t,
-                                       (size_t)pitch * 4, w, (size_t)(n2 + 1),
-                                       hipMemcpyDeviceToHost) != hipSuccess)
-            st = NW_ERR_HIP;
-        if (d_alloc) (void)hipFree(d_alloc);
-        if (d_s1) (void)hipFree(d_s1);
-        if (d_s2) (void)hipFree(d_s2);
-        nw_ctx_destroy(c);
-    }
+    st = host_prepare(h, dev, s1, n1, s2, n2, &d_t, &pitch);
+    if (st == NW_OK) st = nw_fill_device(h.c, h.s1, n1, h.s2, n2, p, d_t, pitch, nullptr, &r);
+    if (st == NW_OK) st = host_copy_back(h, d_t, pitch, n1, n2, host_t + 1, n1 + 2);
     if (st == NW_OK)
         for (int64_t i = 0; i <= n2; ++i) host_t[i * (n1 + 2)] = (int32_t)(n1 + 2);
+    host_trim(h);
     r.status = st;
     if (out) *out = r;
     return st;

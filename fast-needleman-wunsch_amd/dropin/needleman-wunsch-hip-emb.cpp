@@ -11,6 +11,15 @@
 #include "nw_dropin.hpp"
 #include "nw_hip.h"
 
+namespace {
+// device context created at plugin load (see needleman-wunsch-hip.cpp)
+struct Warmup {
+    Warmup() {
+        if (!std::getenv("NW_COLD_START")) (void)nw_host_warmup(-1);
+    }
+} g_warmup;
+}  // namespace
+
 void needlemanWunsch(dnaArray s1, dnaArray s2, int *t) {
     nw_params p;
     nw_params_default(&p);

@@ -35,7 +35,7 @@ EXPORTS = ["nw_params_default", "nw_strerror", "nw_version", "nw_fill", "nw_tabl
            "nw_halo_free", "nw_fill_emb", "nw_sw_align", "nw_sw_traceback", "nw_tuned_shape", "nw_auto_shape", "nw_debug_ctrl", "nw_debug_set_trace",
            "nw_debug_trace_words", "nw_colband_layout", "nw_feed_bytes", "nw_feed_alloc",
            "nw_fill_colband_async", "nw_link_alloc", "nw_link_wait_async", "nw_link_signal_async",
-           "nw_link_status"]
+           "nw_link_status", "nw_host_warmup", "nw_host_release"]
 IPC_HANDLE_BYTES = 64
 
 
@@ -176,6 +176,9 @@ def lib() -> ctypes.CDLL:
     L.nw_link_wait_async.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int32, ctypes.c_void_p]
     L.nw_link_signal_async.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
     L.nw_link_status.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32)]
+    L.nw_host_warmup.argtypes = [ctypes.c_int]
+    L.nw_host_release.argtypes = [ctypes.c_int]
+    L.nw_host_release.restype = None
     L.nw_debug_ctrl.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32)]
     L.nw_debug_set_trace.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     L.nw_debug_trace_words.argtypes = []
@@ -270,6 +273,11 @@ def score(s1, s2, scheme=(1, 0, -1), waves: int = 0, device: int = -1, substrips
     if st != NW_OK:
         raise NwError(st, "nw_fill")
     return int(r.score)
+
+
+def host_release(device: int = -1) -> None:
+    """Free the per-device state of the host-buffer calls (nw_host_release)."""
+    lib().nw_host_release(device)
 
 
 def trace_words() -> int:

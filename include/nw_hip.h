@@ -139,6 +139,20 @@ int nw_fill(const int8_t *s1, int64_t n1, const int8_t *s2, int64_t n2,
             const nw_params *p, int32_t *host_t, nw_result *out);
 
 /*
+ * nw_fill, nw_fill_emb and nw_sw_align keep per-device state between calls: a
+ * context, the device table (kept when at most 16 GiB) and sequence buffers,
+ * and three pinned 128 MiB staging chunks through which the table is copied
+ * back (DMA of the next chunks overlapping the threaded copy of one into
+ * host_t; NW_COPY_THREADS sets the copy threads, default min(16, cores)).
+ * nw_host_warmup(device) creates it ahead of the first call (context, copy
+ * stream, staging; not the table, whose size is not known yet; -1: the current
+ * device); nw_host_release(device) frees it (-1: every device).
+ * NW_HOST_TIMING=1 prints nw_fill's phases (prepare, fill, copy back) to stderr.
+ */
+int nw_host_warmup(int device);
+void nw_host_release(int device);
+
+/*
  * The same fill into the "emb" table layout of the reference's second driver
  * (src/common/driver2.cpp:20-22 allocates (s1.size+2) * (s2.size+1) ints;
  * src/idxarray/idxarray-emb-mt.cpp:4-65 fills it): rows of n1+2 ints, column 0
