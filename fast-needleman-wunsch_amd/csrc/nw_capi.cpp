@@ -775,12 +775,17 @@ struct HostPath {
     int8_t *s1 = nullptr, *s2 = nullptr;
     size_t s1_cap = 0, s2_cap = 0;
     char *stage[3] = {nullptr, nullptr, nullptr};
+    size_t stage_cap = 0;  // bytes per staging chunk
     hipStream_t copy = nullptr;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
 };
 constexpr int kStages = 3;
 
-constexpr size_t kStageBytes = 128u << 20;  // per staging chunk
+// staging chunk: up to 256 MiB (a third of the table, at least 16 MiB), pinned
+// with hipHostMallocCoherent (tools/d2h_bench.cpp on the box: 40 GB through 3 x
+// 256 MiB coherent chunks and 8 copy threads at 56.6 GB/s, the bare pinned
+// hipMemcpy2D's 56.4; 128 MiB default-flag chunks 45-53)
+constexpr size_t kStageMax = 256u << 20, kStageMin = 16u << 20;
 // tables up to this size stay cached between calls; a larger one is released
 // when its call returns (it would crowd out the caller's own device work)
 constexpr size_t kKeepTableBytes = 16ull << 30;
@@ -805,6 +810,7 @@ void host_free(HostPath &h) {
         h.stage[k] = nullptr;
         h.ev[k] = nullptr;
     }
+    h.stage_cap = 0;
     if (h.copy) (void)hipStreamDestroy(h.copy);
     nw_ctx_destroy(h.c);
     h.c = nullptr;
@@ -852,17 +858,26 @@ void par_memcpy(char *dst, const char *src, size_t bytes, int threads) {
 
 int copy_threads() {
     if (const char *e = std::getenv("NW_COPY_THREADS")) return std::max(1, std::atoi(e));
-    return (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
+    return (int)std::min<unsigned>(8u, std::max(1u, std::thread::hardware_concurrency()));
 }
 
 // Rows 0..n2 (n1 + 1 int32 each) of the device table into host rows of
 // `stride` int32 (the reference layout: stride = n1 + 1), through the pinned
 // staging chunks.
-int host_staging(HostPath &h) {
-    for (int k = 0; k < kStages; ++k) {
-        if (!h.stage[k]) NW_HIP_TRY(hipHostMalloc((void **)&h.stage[k], kStageBytes, 0));
-        if (!h.ev[k]) NW_HIP_TRY(hipEventCreateWithFlags(&h.ev[k], hipEventDisableTiming));
+int host_staging(HostPath &h, size_t table_bytes) {
+    size_t want = std::min(kStageMax, std::max(kStageMin, (table_bytes / kStages + (2u << 20) - 1) & ~((size_t)(2u << 20) - 1)));
+    if (want > h.stage_cap) {
+        for (int k = 0; k < kStages; ++k) {
+            if (h.stage[k]) (void)hipHostFree(h.stage[k]);
+            h.stage[k] = nullptr;
+        }
+        h.stage_cap = 0;
+        for (int k = 0; k < kStages; ++k)
+            NW_HIP_TRY(hipHostMalloc((void **)&h.stage[k], want, hipHostMallocCoherent));
+        h.stage_cap = want;
     }
+    for (int k = 0; k < kStages; ++k)
+        if (!h.ev[k]) NW_HIP_TRY(hipEventCreateWithFlags(&h.ev[k], hipEventDisableTiming));
     if (!h.copy) NW_HIP_TRY(hipStreamCreateWithFlags(&h.copy, hipStreamNonBlocking));
     return NW_OK;
 }
@@ -870,11 +885,11 @@ int host_staging(HostPath &h) {
 int host_copy_back(HostPath &h, const int32_t *d_t, int64_t pitch, int64_t n1, int64_t n2, int32_t *host,
                    int64_t stride) {
     int st;
-    if ((st = host_staging(h)) != NW_OK) return st;
     const size_t w = (size_t)(n1 + 1) * 4;
     const int64_t rows = n2 + 1;
-    const int64_t rpc = std::max<int64_t>(1, (int64_t)(kStageBytes / w));
-    if ((size_t)rpc * w > kStageBytes) {  // one row wider than a chunk: direct
+    if ((st = host_staging(h, w * (size_t)rows)) != NW_OK) return st;
+    const int64_t rpc = std::max<int64_t>(1, (int64_t)(h.stage_cap / w));
+    if ((size_t)rpc * w > h.stage_cap) {  // one row wider than a chunk: direct
         NW_HIP_TRY(hipMemcpy2D(host, (size_t)stride * 4, d_t, (size_t)pitch * 4, w, (size_t)rows,
                                hipMemcpyDeviceToHost));
         return NW_OK;
@@ -889,8 +904,14 @@ int host_copy_back(HostPath &h, const int32_t *d_t, int64_t pitch, int64_t n1, i
     };
     // the fill ran on the null stream (synchronous), so the copy stream sees the table
     for (int64_t ch = 0; ch < std::min<int64_t>(kStages, nch); ++ch) NW_HIP_TRY(issue(ch));
+    double t_dma = 0, t_cpy = 0;
+    auto tnow = [] { return std::chrono::steady_clock::now(); };
+    auto sec = [](auto a, auto b) { return std::chrono::duration<double>(b - a).count(); };
     for (int64_t ch = 0; ch < nch; ++ch) {
+        const auto a0 = tnow();
         NW_HIP_TRY(hipEventSynchronize(h.ev[ch % kStages]));
+        const auto a1 = tnow();
+        t_dma += sec(a0, a1);
         const int64_t r0 = ch * rpc, nr = std::min(rpc, rows - r0);
         const char *src = h.stage[ch % kStages];
         if (stride * 4 == (int64_t)w) {
@@ -898,8 +919,12 @@ int host_copy_back(HostPath &h, const int32_t *d_t, int64_t pitch, int64_t n1, i
         } else {
             for (int64_t r = 0; r < nr; ++r) std::memcpy(host + (r0 + r) * stride, src + (size_t)r * w, w);
         }
+        t_cpy += sec(a1, tnow());
         if (ch + kStages < nch) NW_HIP_TRY(issue(ch + kStages));
     }
+    if (std::getenv("NW_HOST_TIMING"))
+        std::fprintf(stderr, "  copy back: %lld chunks of %zu MiB, %d threads: waiting on DMA %.1f ms, copying %.1f ms\n",
+                     (long long)nch, h.stage_cap >> 20, threads, t_dma * 1e3, t_cpy * 1e3);
     return NW_OK;
 }
 
@@ -921,7 +946,7 @@ int nw_host_warmup(int device) {
     int st;
     if (!h.c && (st = nw_ctx_create(dev, &h.c)) != NW_OK) return st;
     NW_HIP_TRY(hipSetDevice(dev));
-    return host_staging(h);
+    return host_staging(h, kStageMax * kStages);
 }
 
 void nw_host_release(int device) {

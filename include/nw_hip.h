@@ -141,9 +141,9 @@ int nw_fill(const int8_t *s1, int64_t n1, const int8_t *s2, int64_t n2,
 /*
  * nw_fill, nw_fill_emb and nw_sw_align keep per-device state between calls: a
  * context, the device table (kept when at most 16 GiB) and sequence buffers,
- * and three pinned 128 MiB staging chunks through which the table is copied
- * back (DMA of the next chunks overlapping the threaded copy of one into
- * host_t; NW_COPY_THREADS sets the copy threads, default min(16, cores)).
+ * and three pinned staging chunks (up to 256 MiB each) through which the
+ * table is copied back (DMA of the next chunks overlapping the threaded copy of
+ * one into host_t; NW_COPY_THREADS sets the copy threads, default min(8, cores)).
  * nw_host_warmup(device) creates it ahead of the first call (context, copy
  * stream, staging; not the table, whose size is not known yet; -1: the current
  * device); nw_host_release(device) frees it (-1: every device).

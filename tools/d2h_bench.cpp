@@ -56,9 +56,49 @@ int main(int argc, char **argv) {
     int32_t *host = new int32_t[(size_t)cols * rows];
     for (size_t i = 0; i < (size_t)cols * rows; i += 1024) host[i] = 0;
 
-    double t0 = now();
+    double t0, t1;
+    if (argc > 4 && atoi(argv[4]) == 1) {
+        // the drop-in's configuration on a caller buffer fresh from the touch loop,
+        // twice: cold pages first, then the same buffer again; then a memcpy-only pass
+        char *st[3];
+        hipEvent_t ev[3];
+        hipStream_t s;
+        CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        for (int k = 0; k < 3; ++k) {
+            CK(hipHostMalloc((void **)&st[k], chunk, hipHostMallocCoherent));
+            CK(hipEventCreateWithFlags(&ev[k], hipEventDisableTiming));
+        }
+        const long rpc = std::max<long>(1, (long)(chunk / w));
+        const long nch = (rows + rpc - 1) / rpc;
+        for (int pass = 0; pass < 2; ++pass) {
+            double tdma = 0, tcpy = 0;
+            t0 = now();
+            auto issue = [&](long c) {
+                const long r0 = c * rpc, nr = std::min(rpc, rows - r0);
+                CK(hipMemcpy2DAsync(st[c % 3], w, d + r0 * pitch, pitch * 4, w, nr, hipMemcpyDeviceToHost, s));
+                CK(hipEventRecord(ev[c % 3], s));
+            };
+            for (long c = 0; c < std::min<long>(3, nch); ++c) issue(c);
+            for (long c = 0; c < nch; ++c) {
+                double a0 = now();
+                CK(hipEventSynchronize(ev[c % 3]));
+                double a1 = now();
+                const long r0 = c * rpc, nr = std::min(rpc, rows - r0);
+                par_copy((char *)host + (size_t)r0 * w, st[c % 3], (size_t)nr * w, threads);
+                double a2 = now();
+                tdma += a1 - a0;
+                tcpy += a2 - a1;
+                if (c + 3 < nch) issue(c + 3);
+            }
+            t1 = now();
+            std::printf("fresh-first pass %d: %.3f s %.1f GB/s (waiting on DMA %.3f s, copying %.3f s)\n", pass,
+                        t1 - t0, bytes / (t1 - t0) / 1e9, tdma, tcpy);
+        }
+        return 0;
+    }
+    t0 = now();
     CK(hipMemcpy2D(host, w, d, pitch * 4, w, rows, hipMemcpyDeviceToHost));
-    double t1 = now();
+    t1 = now();
     std::printf("pageable2d  %.3f s  %.1f GB/s\n", t1 - t0, bytes / (t1 - t0) / 1e9);
 
     {
@@ -90,37 +130,65 @@ int main(int argc, char **argv) {
                         t1 - t0, t2 - t1, bytes / (t2 - t1) / 1e9, t3 - t2);
         }
     }
-    for (int nb : {2, 3}) {
-        std::vector<char *> st(nb);
-        std::vector<hipEvent_t> ev(nb);
-        hipStream_t s;
-        CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-        for (int k = 0; k < nb; ++k) {
-            CK(hipHostMalloc((void **)&st[k], chunk, 0));
-            CK(hipEventCreateWithFlags(&ev[k], hipEventDisableTiming));
+    struct Flag {
+        const char *name;
+        unsigned f;
+    } flags[] = {{"default", hipHostMallocDefault}, {"noncoherent", hipHostMallocNonCoherent},
+                 {"coherent", hipHostMallocCoherent}};
+    for (const Flag &fl : flags) {
+        // CPU side alone: memcpy out of one pinned chunk into the caller's buffer
+        {
+            char *pin = nullptr;
+            CK(hipHostMalloc((void **)&pin, chunk, fl.f));
+            std::memset(pin, 1, chunk);
+            for (int th : {8, 16}) {
+                const long reps = (long)(bytes / chunk);
+                t0 = now();
+                for (long r = 0; r < reps; ++r) par_copy((char *)host + (size_t)r * chunk, pin, chunk, th);
+                t1 = now();
+                std::printf("  %-11s memcpy only, %2d threads: %.1f GB/s\n", fl.name, th,
+                            reps * (double)chunk / (t1 - t0) / 1e9);
+            }
+            CK(hipHostFree(pin));
         }
-        const long rpc = std::max<long>(1, (long)(chunk / w));
-        const long nch = (rows + rpc - 1) / rpc;
-        t0 = now();
-        auto issue = [&](long c) {
-            const long r0 = c * rpc, nr = std::min(rpc, rows - r0);
-            CK(hipMemcpy2DAsync(st[c % nb], w, d + r0 * pitch, pitch * 4, w, nr, hipMemcpyDeviceToHost, s));
-            CK(hipEventRecord(ev[c % nb], s));
-        };
-        for (long c = 0; c < std::min<long>(nb, nch); ++c) issue(c);
-        for (long c = 0; c < nch; ++c) {
-            CK(hipEventSynchronize(ev[c % nb]));
-            const long r0 = c * rpc, nr = std::min(rpc, rows - r0);
-            par_copy((char *)host + (size_t)r0 * w, st[c % nb], (size_t)nr * w, threads);
-            if (c + nb < nch) issue(c + nb);
+        for (int th : {8, 16}) {
+            for (size_t ck : {chunk / 2, chunk, chunk * 2}) {
+                for (int nb : {3, 4}) {
+                    std::vector<char *> st(nb);
+                    std::vector<hipEvent_t> ev(nb);
+                    hipStream_t s;
+                    CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+                    for (int k = 0; k < nb; ++k) {
+                        CK(hipHostMalloc((void **)&st[k], ck, fl.f));
+                        CK(hipEventCreateWithFlags(&ev[k], hipEventDisableTiming));
+                    }
+                    const long rpc = std::max<long>(1, (long)(ck / w));
+                    const long nch = (rows + rpc - 1) / rpc;
+                    t0 = now();
+                    auto issue = [&](long c) {
+                        const long r0 = c * rpc, nr = std::min(rpc, rows - r0);
+                        CK(hipMemcpy2DAsync(st[c % nb], w, d + r0 * pitch, pitch * 4, w, nr, hipMemcpyDeviceToHost,
+                                            s));
+                        CK(hipEventRecord(ev[c % nb], s));
+                    };
+                    for (long c = 0; c < std::min<long>(nb, nch); ++c) issue(c);
+                    for (long c = 0; c < nch; ++c) {
+                        CK(hipEventSynchronize(ev[c % nb]));
+                        const long r0 = c * rpc, nr = std::min(rpc, rows - r0);
+                        par_copy((char *)host + (size_t)r0 * w, st[c % nb], (size_t)nr * w, th);
+                        if (c + nb < nch) issue(c + nb);
+                    }
+                    t1 = now();
+                    std::printf("staged %-11s th %2d chunk %4zu MB x%d  %.3f s  %.1f GB/s\n", fl.name, th, ck >> 20,
+                                nb, t1 - t0, bytes / (t1 - t0) / 1e9);
+                    for (int k = 0; k < nb; ++k) {
+                        CK(hipHostFree(st[k]));
+                        CK(hipEventDestroy(ev[k]));
+                    }
+                    CK(hipStreamDestroy(s));
+                }
+            }
         }
-        t1 = now();
-        std::printf("staged x%d  %.3f s  %.1f GB/s\n", nb, t1 - t0, bytes / (t1 - t0) / 1e9);
-        for (int k = 0; k < nb; ++k) {
-            CK(hipHostFree(st[k]));
-            CK(hipEventDestroy(ev[k]));
-        }
-        CK(hipStreamDestroy(s));
     }
     long bad = 0;
     for (size_t i = 0; i < (size_t)cols * rows; i += 4099)

