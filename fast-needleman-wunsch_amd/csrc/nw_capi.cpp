@@ -43,7 +43,9 @@ struct nw_ctx {
     size_t smax_cap = 0;
     uint8_t *ops = nullptr;     // SW traceback ops (device)
     size_t ops_cap = 0;
-    int64_t *swinfo = nullptr;  // SW traceback info (4 words) + locate key
+    int64_t *swinfo = nullptr;  // SW locate key ([12])
+    void *tbscratch = nullptr;  // SW traceback windows (nw::sw_tb_scratch_bytes)
+    size_t tbscratch_cap = 0;
     int last_col0 = 0;
     int last_kernel = NW_KERNEL_STRIPS;
 };
@@ -310,6 +312,7 @@ void nw_ctx_destroy(nw_ctx *c) {
     if (c->smax) (void)hipFree(c->smax);
     if (c->ops) (void)hipFree(c->ops);
     if (c->swinfo) (void)hipFree(c->swinfo);
+    if (c->tbscratch) (void)hipFree(c->tbscratch);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     delete c;
@@ -721,20 +724,28 @@ int nw_sw_traceback(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *d_s
     int st;
     const size_t need = (size_t)std::max<int64_t>(end_i + end_j + 1, 1);
     if ((st = grow((void **)&c->ops, &c->ops_cap, need)) != NW_OK) return st;
-    if (!c->swinfo) NW_HIP_TRY(hipMalloc(&c->swinfo, 16 * sizeof(int64_t)));  // [0..9] traceback info, [12] locate key
+    // window geometry: band half-width and windows per round (NW_TB_BAND /
+    // NW_TB_MAXWIN override them: narrow bands and short rounds for the tests)
+    int32_t band = nw::kTbBandDefault, maxwin = nw::kTbMaxWinDefault;
+    if (const char *e = std::getenv("NW_TB_BAND")) band = std::max(1, std::min(128, std::atoi(e)));
+    if (const char *e = std::getenv("NW_TB_MAXWIN")) maxwin = std::max(1, std::atoi(e));
+    maxwin = (int32_t)std::min<int64_t>(maxwin, end_i / 64 + 1);
+    if ((st = grow((void **)&c->tbscratch, &c->tbscratch_cap, nw::sw_tb_scratch_bytes(maxwin, band))) != NW_OK)
+        return st;
     NW_HIP_TRY(hipEventRecord(c->ev0, nullptr));
-    if (nw::launch_sw_traceback(d_t, pitch, n1, (const uint8_t *)d_s1, (const uint8_t *)d_s2, p->match, p->mismatch,
-                                p->gap, end_i, end_j, c->ops, (int64_t)need, c->swinfo, nullptr) != hipSuccess)
-        return NW_ERR_HIP;
-    NW_HIP_TRY(hipEventRecord(c->ev1, nullptr));
     int64_t info[10];
-    NW_HIP_TRY(hipMemcpy(info, c->swinfo, sizeof info, hipMemcpyDeviceToHost));
-    if (std::getenv("NW_TB_DEBUG"))  // traceback phase timers (s_memrealtime ticks)
-        std::fprintf(stderr,
-                     "nw_sw_traceback: windows %lld, load %.3f ms, classify %.3f ms (1-step %.3f, 2-step %.3f), "
-                     "walk %.3f ms\n",
-                     (long long)info[7], info[4] * 1e-5, info[5] * 1e-5, info[8] * 1e-5, info[9] * 1e-5,
-                     info[6] * 1e-5);
+    const int he = nw::run_sw_traceback(d_t, pitch, n1, (const uint8_t *)d_s1, (const uint8_t *)d_s2, p->match,
+                                        p->mismatch, p->gap, end_i, end_j, c->ops, (int64_t)need, c->tbscratch,
+                                        maxwin, band, info, nullptr);
+    if (he != hipSuccess) {
+        std::fprintf(stderr, "libnwhip: SW traceback failed: %s\n", hipGetErrorString((hipError_t)he));
+        return NW_ERR_HIP;
+    }
+    NW_HIP_TRY(hipEventRecord(c->ev1, nullptr));
+    NW_HIP_TRY(hipEventSynchronize(c->ev1));
+    if (std::getenv("NW_TB_DEBUG"))
+        std::fprintf(stderr, "nw_sw_traceback: %lld moves, %lld rounds, %lld windows (band %d)\n", (long long)info[0],
+                     (long long)info[4], (long long)info[5], band);
     float ms = 0.f;
     NW_HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
     std::memset(out, 0, sizeof *out);

@@ -78,12 +78,17 @@ int launch_colband_edge(const uint64_t *feed, int32_t *table, int64_t pitch, int
 int launch_sw_locate(const int32_t *table, int64_t pitch, int64_t n1, int64_t n2, int64_t col0,
                      int32_t strip_cols, const int32_t *smax, int32_t nstrips, uint64_t *key, int32_t *best,
                      void *stream);
-// traceback from (end_i, end_j) (see nw_fill.hip nw_sw_traceback); ops[] gets one
-// byte per step from the end cell back (0 diag, 1 up, 2 left), info8[0] = steps,
-// [1] = begin row, [2] = begin column, [3] = status (0 ok, 1 ops buffer too small)
-int launch_sw_traceback(const int32_t *table, int64_t pitch, int64_t n1, const uint8_t *s1, const uint8_t *s2,
-                        int32_t match, int32_t mismatch, int32_t gap, int64_t end_i, int64_t end_j,
-                        uint8_t *ops, int64_t ops_cap, int64_t *info, void *stream);
+// traceback from (end_i, end_j), parallel over row windows (nw_sw.hip): ops[]
+// gets one byte per move from the end cell back (0 diag, 1 up, 2 left); host
+// info[0] = moves, [1..2] = begin cell, [3] = status (0 ok, 1 ops buffer too
+// small, 2 not a Smith-Waterman table), [4] rounds, [5] windows.  Synchronises
+// `stream` once per round.  scratch: sw_tb_scratch_bytes(maxwin, band) bytes.
+size_t sw_tb_scratch_bytes(int32_t maxwin, int32_t band);
+int run_sw_traceback(const int32_t *table, int64_t pitch, int64_t n1, const uint8_t *s1, const uint8_t *s2,
+                     int32_t match, int32_t mismatch, int32_t gap, int64_t end_i, int64_t end_j, uint8_t *ops,
+                     int64_t ops_cap, void *scratch, int32_t maxwin, int32_t band, int64_t *info, void *stream);
+constexpr int32_t kTbBandDefault = 128;    // band half-width of the traceback windows
+constexpr int32_t kTbMaxWinDefault = 4096; // windows per round (64 rows each)
 
 // Launch helpers implemented in nw_fill.hip.  Return hipError_t as int.
 // charmap of s1 into meta, then the row packs (mapped when perm allows it)

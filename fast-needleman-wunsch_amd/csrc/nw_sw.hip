@@ -37,44 +37,45 @@ __global__ __launch_bounds__(256) void nw_sw_best(const int32_t *__restrict__ sm
     }
 }
 
-// First row-major cell holding the best value: workgroup (p, y) scans strip /
-// panel p's columns (any width: 256 at a time) over the row blocks y, y +
-// gridDim.y, ... of kLocRows rows if the strip's maximum is the best one; each
-// thread keeps the first row of its column, the workgroup and then the grid take
-// the minimum key (row << 32 | column).  gridDim.y is capped (the y dimension of
-// a grid is limited), tall tables loop.
-constexpr int kLocRows = 512;
-constexpr int kLocMaxY = 4096;
+// First row-major cell holding the best value: workgroup y scans row blocks y,
+// y + gridDim.x, ... of kLocRows rows in every strip / panel (any width: 256
+// columns at a time) whose maximum is the best one -- a column's kLocRows loads
+// are unconditional and independent, the first match is picked after -- and the
+// workgroup and then the grid take the minimum key (row << 32 | column).
+constexpr int kLocRows = 64;
+constexpr int kLocMaxGrid = 4096;
 __global__ __launch_bounds__(256) void nw_sw_locate(const int32_t *__restrict__ table, int64_t pitch,
                                                     int64_t n1, int64_t n2, int64_t col0, int32_t strip_cols,
-                                                    const int32_t *__restrict__ smax,
+                                                    const int32_t *__restrict__ smax, int32_t nstrips,
                                                     const int32_t *__restrict__ best,
                                                     uint64_t *__restrict__ key) {
-    const int32_t p = blockIdx.x;
     const int32_t b = *best;
-    if (b <= 0 || smax[p] != b) return;
+    if (b <= 0) return;
     __shared__ unsigned long long kmin;
     if (threadIdx.x == 0) kmin = ~0ull;
     __syncthreads();
     const int64_t nblk = (n2 + kLocRows) / kLocRows;
-    for (int64_t y = blockIdx.y; y < nblk; y += gridDim.y) {
+    for (int64_t y = blockIdx.x; y < nblk; y += gridDim.x) {
         const int64_t r0 = y * kLocRows;
-        const int64_t r1 = min(r0 + kLocRows, n2 + 1);
-        for (int32_t x = threadIdx.x; x < strip_cols; x += 256) {
-            const int64_t c = col0 + (int64_t)p * strip_cols + x;
-            if (c > n1) break;
-            for (int64_t r = r0; r < r1; ++r) {
-                if (table[r * pitch + c] == b) {
-                    atomicMin(&kmin, ((unsigned long long)r << 32) | (unsigned long long)c);
-                    break;
+        const int nr = (int)min((int64_t)kLocRows, n2 + 1 - r0);
+        for (int32_t p = 0; p < nstrips; ++p) {
+            if (smax[p] != b) continue;
+            for (int32_t x = threadIdx.x; x < strip_cols; x += 256) {
+                const int64_t c = col0 + (int64_t)p * strip_cols + x;
+                if (c > n1) break;
+                const int32_t *col = table + r0 * pitch + c;
+                int first = kLocRows;
+#pragma unroll 16
+                for (int rr = kLocRows - 1; rr >= 0; --rr) {
+                    const int32_t v = rr < nr ? col[rr * pitch] : 0;
+                    first = v == b ? rr : first;
                 }
+                if (first < kLocRows)
+                    atomicMin(&kmin, ((unsigned long long)(r0 + first) << 32) | (unsigned long long)c);
             }
         }
-        // a later row block cannot hold an earlier row: stop once one matched
-        __syncthreads();
-        if (kmin != ~0ull) break;
-        __syncthreads();
     }
+    __syncthreads();
     if (threadIdx.x == 0 && kmin != ~0ull) atomicMin((unsigned long long *)key, kmin);
 }
 
@@ -83,215 +84,220 @@ int launch_sw_locate(const int32_t *table, int64_t pitch, int64_t n1, int64_t n2
                      void *stream) {
     hipStream_t s = (hipStream_t)stream;
     hipLaunchKernelGGL(nw_sw_best, dim3(1), dim3(256), 0, s, smax, nstrips, best, key);
-    const int64_t rb = std::min<int64_t>((n2 + kLocRows) / kLocRows, kLocMaxY);
-    hipLaunchKernelGGL(nw_sw_locate, dim3((unsigned)nstrips, (unsigned)rb), dim3(256), 0, s, table, pitch, n1, n2,
-                       col0, strip_cols, smax, best, key);
+    const int64_t grid = std::min<int64_t>((n2 + kLocRows) / kLocRows, kLocMaxGrid);
+    hipLaunchKernelGGL(nw_sw_locate, dim3((unsigned)grid), dim3(256), 0, s, table, pitch, n1, n2, col0, strip_cols,
+                       smax, nstrips, best, key);
     return (int)hipGetLastError();
 }
 
-// Traceback: one workgroup of 1024 threads.  The table around the current cell
-// (i, j) is staged in LDS a window at a time: a band of kBandW = 2B+1 cells around
-// the diagonal through (i, j) (the "entry diagonal"), over up to kBandR rows --
-// window cell (r, x) is table cell (i0 + r, j - (rows-1-r) + x - B).  A diagonal
-// move keeps x, up moves to x + 1, left to x - 1, so the three moves are the LDS
-// index steps W, W - 1 and 1.  Smith-Waterman paths are mostly diagonal, so a band
-// covers ~kBandR moves per window where a square window of the same LDS covers ~W.
-// Every thread issues all its loads before it waits; all threads then classify
-// every cell of the window with the move the walk takes there, stored as its
-// index step (diag if t == t[i-1][j-1] + s; else up if t == t[i-1][j] + GAP; else
-// left if t == t[i][j-1] + GAP), or a stop code: t == 0 (or row / column 0 of the
-// table), the window's top row or band side (the walk continues in the next
-// window from there), or "no move matches" (not a Smith-Waterman table).
-// Doubling passes turn the codes into 4-move codes and thread 0 follows them --
-// per 4 moves one dependent LDS read, the ops into an LDS buffer -- and all
-// threads copy the window's ops out together.
-constexpr int kBandB = 32;
-constexpr int kBandW = 2 * kBandB + 1;          // 65 cells per window row
-constexpr int kBandR = 252;                     // rows per window: 252 * 65 <= 16384 cells
-constexpr int kTbThreads = 1024;
-constexpr int kTbCells = kBandR * kBandW;
-constexpr int kTbPer = (kTbCells + kTbThreads - 1) / kTbThreads;  // cells per thread
-constexpr int kTbPad = kTbPer * kTbThreads;  // LDS arrays padded: no bounds checks (rows >= kBandR there)
-constexpr uint8_t kMvLeft = 1, kMvUp = kBandW - 1, kMvDiag = kBandW;  // index steps
-constexpr uint8_t kStop = 0, kEdge = 200, kBad = 255;
-__global__ __launch_bounds__(kTbThreads) void nw_sw_traceback(
-    const int32_t *__restrict__ table, int64_t pitch, int64_t n1, const uint8_t *__restrict__ s1,
-    const uint8_t *__restrict__ s2, int32_t match, int32_t mismatch, int32_t gap, int64_t end_i, int64_t end_j,
-    uint8_t *__restrict__ ops, int64_t ops_cap, int64_t *__restrict__ info) {
-    constexpr int W = kBandW, B = kBandB;
-    __shared__ int32_t win[kTbPad];
-    __shared__ uint8_t code[kTbPad];
-    __shared__ uint16_t cc2[kTbPad];
-    __shared__ uint16_t ob[kBandR / 2 + kBandW + 2];  // the window's moves, 4 per entry (2 bits each | count << 8)
-    __shared__ uint8_t c1[kBandR + kBandW], c2[kBandR];
-    __shared__ int64_t st[5];  // i, j, steps, status (done flag in the sign of i), moves this window
+// Traceback, parallel over windows.  The path from the best cell runs up and
+// left through cells with t > 0, taking at every cell the first move that
+// reproduces t (diag, then up, then left -- the order of serial.cpp:24-30's max).
+// A ROUND from a start cell (is, js) cuts the rows above it into WINDOWS of kTbR
+// rows, all skewed onto the diagonal through (is, js): window k's cell (r, x) is
+// table cell (i0 + r, dj + r + x), i0 = is - (k+1) kTbR + 1, dj = js - is + i0 - B,
+// x in [0, 2B], so a diagonal move keeps x, up is x + 1, left x - 1, and window
+// k+1's bottom row continues window k's top row at the same x.
+//   nw_tb_windows (one workgroup per window, all at once): the move code of every
+//     cell (from the table, L2-resident neighbours), kept for nw_tb_emit, and for
+//     every entry x of the bottom row the EXIT of the path from there: out of the
+//     top at x' (continue in window k+1), a stop (t = 0, row / column 0: the
+//     path's first cell), a move out of the band (the round restarts from that
+//     cell, re-centred), or no matching move (not a Smith-Waterman table);
+//   nw_tb_chain (one workgroup): follows the exits window to window from x = B --
+//     one LDS read per window, exit tables staged kChain windows at a time --
+//     giving each window its entry and its ops offset;
+//   nw_tb_emit (one workgroup per window): walks its window from its entry and
+//     writes the ops at its offset.
+// A path that drifts more than B columns off the round's diagonal costs another
+// round (re-centred at the cell where it left); run_sw_traceback loops rounds.
+constexpr int kTbR = 64;                     // rows per window
+constexpr int kTbBMax = 128;                 // band half-width B <= kTbBMax
+constexpr int kTbWMax = 2 * kTbBMax + 1;     // cells per window row, W = 2B + 1
+constexpr int kTbThreads = 512;
+constexpr int kChain = 32;                   // windows per LDS chunk of nw_tb_chain
+enum : uint8_t { kCStop = 0, kCDiag = 1, kCUp = 2, kCLeft = 3, kCBad = 4 };
+enum : uint32_t { kXCont = 0, kXStop = 1, kXOut = 2, kXBad = 3 };
+// exit record: kind 0-1 | moves 2-11 | row 12-18 | column 19-27 (kXCont: the
+// column entered in the next window; otherwise the cell where the walk ended)
+__device__ __forceinline__ uint32_t xrec(uint32_t kind, uint32_t cnt, uint32_t r, uint32_t x) {
+    return kind | (cnt << 2) | (r << 12) | (x << 19);
+}
+
+// One window's walk from entry x (row kTbR - 1) over its move codes cd[]: calls
+// emit(op) per move (0 diag, 1 up, 2 left); returns the exit record.
+template <typename F>
+__device__ __forceinline__ uint32_t tb_walk(const uint8_t *cd, int W, int x, F &&emit) {
+    int r = kTbR - 1;
+    uint32_t cnt = 0;
+    for (;;) {
+        const uint8_t c = cd[r * W + x];
+        if (c == kCStop) return xrec(kXStop, cnt, r, x);
+        if (c == kCBad) return xrec(kXBad, cnt, r, x);
+        const int nx = c == kCUp ? x + 1 : c == kCLeft ? x - 1 : x;
+        if (nx < 0 || nx >= W) return xrec(kXOut, cnt, r, x);  // (the move is the next round's)
+        emit(c == kCDiag ? 0u : c == kCUp ? 1u : 2u);
+        ++cnt;
+        if (c != kCLeft && r == 0) return xrec(kXCont, cnt, 0, nx);
+        r = c == kCLeft ? r : r - 1;
+        x = nx;
+    }
+}
+
+__global__ __launch_bounds__(kTbThreads) void nw_tb_windows(const int32_t *__restrict__ table, int64_t pitch,
+                                                            int64_t n1, const uint8_t *__restrict__ s1,
+                                                            const uint8_t *__restrict__ s2, int32_t match,
+                                                            int32_t mismatch, int32_t gap, int64_t is, int64_t js,
+                                                            int32_t B, uint8_t *__restrict__ codes,
+                                                            uint32_t *__restrict__ exits) {
+    __shared__ uint8_t cd[kTbR * kTbWMax];
+    const int W = 2 * B + 1;
+    const int k = blockIdx.x;
+    const int64_t i0 = is - (int64_t)(k + 1) * kTbR + 1;
+    const int64_t dj = js - is + i0 - B;
+    const int ncell = kTbR * W;
+    uint8_t *gcd = codes + (int64_t)k * ncell;
+#pragma unroll 4
+    for (int e = threadIdx.x; e < ncell; e += kTbThreads) {
+        const int r = e / W, x = e - r * W;
+        const int64_t i = i0 + r, j = dj + r + x;
+        const bool in = i >= 1 && j >= 1 && j <= n1;
+        // loads from clamped addresses (issued together), the decision after
+        const int64_t ic = in ? i : 1, jc = in ? j : 1;
+        const int32_t *row = table + ic * pitch;
+        const int32_t t = row[jc], td = row[jc - 1 - pitch], tu = row[jc - pitch], tl = row[jc - 1];
+        const int32_t sc = s1[jc - 1] == s2[ic - 1] ? match : mismatch;
+        uint8_t c = kCStop;
+        if (in && t > 0) c = t == td + sc ? kCDiag : t == tu + gap ? kCUp : t == tl + gap ? kCLeft : kCBad;
+        cd[e] = c;
+        gcd[e] = c;
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < W) exits[(int64_t)k * W + threadIdx.x] = tb_walk(cd, W, threadIdx.x, [](uint32_t) {});
+}
+
+// ctl: [0] ops so far, [1] how the round ended (kXStop / kXCont|kXOut = restart /
+// kXBad / 4 = ops buffer too small), [2..3] the begin cell or the restart cell,
+// [4] windows holding ops this round.  wentry[k] = {entry x, ops offset}.
+__global__ __launch_bounds__(1024) void nw_tb_chain(const uint32_t *__restrict__ exits, int32_t nwin, int32_t B,
+                                                    int64_t is, int64_t js, int64_t ops_cap,
+                                                    int64_t *__restrict__ wentry, int64_t *__restrict__ ctl) {
+    __shared__ uint32_t ex[kChain * kTbWMax];
+    __shared__ int64_t st[3];  // entry x, ops offset, done
+    const int W = 2 * B + 1;
     const int tid = threadIdx.x;
     if (tid == 0) {
-        st[0] = end_i;
-        st[1] = end_j;
+        st[0] = B;
+        st[1] = ctl[0];
         st[2] = 0;
-        st[3] = 0;
-        st[4] = 0;
     }
-    __syncthreads();
-    uint64_t tl = 0, tc = 0, tw = 0, nwin = 0;  // (thread 0) ticks loading / classifying / walking
-    uint64_t tc1 = 0, tc2 = 0;                  // (of tc: the 1-step codes, the 2-step codes)
-    for (;;) {
-        const int64_t i = st[0], j = st[1];
-        if (i <= 0 || j <= 0 || st[3] != 0) break;
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        ++nwin;
-        const int rows = (int)(i + 1 < kBandR ? i + 1 : kBandR);
-        const int64_t i0 = i - (rows - 1);
-        const int64_t jb = j - (rows - 1) - B;  // table column of window cell (r, x) = jb + r + x
-        // r + x ranges over [0, kBandR + kBandW): the table's columns 1 and n1 as
-        // offsets from jb, clamped into that range (32-bit compares in the classify pass)
-        const int lo1 = (int)std::min<int64_t>(std::max<int64_t>(1 - jb, -1), kBandR + kBandW);
-        const int hi = (int)std::min<int64_t>(std::max<int64_t>(n1 - jb, -1), kBandR + kBandW);
-        int32_t v[kTbPer];
-#pragma unroll
-        for (int k = 0; k < kTbPer; ++k) {
-            const int e = tid + k * kTbThreads, r = e / W, x = e % W;
-            const int64_t gj = jb + r + x;
-            v[k] = (e < kTbCells && r < rows && gj >= 0 && gj <= n1) ? table[(i0 + r) * pitch + gj] : 0;
-        }
-#pragma unroll
-        for (int k = 0; k < kTbPer; ++k) {
-            const int e = tid + k * kTbThreads;
-            if (e < kTbCells) win[e] = v[k];
-        }
-        if (tid < kBandR + kBandW) {  // c1[r + x] = s1 character of column jb + r + x
-            const int64_t gj = jb + tid;
-            c1[tid] = (gj >= 1 && gj <= n1) ? s1[gj - 1] : 0;
-        }
-        if (tid < kBandR) c2[tid] = (tid < rows && i0 + tid >= 1) ? s2[i0 + tid - 1] : 0;
+    for (int k0 = 0; k0 < nwin; k0 += kChain) {
+        const int nk = min(kChain, nwin - k0);
+        for (int e = tid; e < nk * W; e += 1024) ex[e] = exits[(int64_t)k0 * W + e];
         __syncthreads();
-        const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
-        #pragma unroll
-        for (int kk = 0; kk < kTbPer; ++kk) {
-            const int e = tid + kk * kTbThreads;
-            const int r = e / W, x = e - r * W, q = r + x;
-            uint8_t cd = kStop;
-            if (r >= rows || q < lo1 || q > hi || i0 + r == 0) {
-                cd = kStop;  // (outside the table, or its row / column 0)
-            } else if (r == 0 || x == 0 || x == W - 1) {
-                cd = kEdge;  // a neighbour lies outside the window
-            } else {
-                const int32_t t = win[e];
-                if (t > 0) {
-                    const int32_t sc = c1[q] == c2[r] ? match : mismatch;
-                    cd = t == win[e - W] + sc        ? kMvDiag
-                         : t == win[e - W + 1] + gap ? kMvUp
-                         : t == win[e - 1] + gap     ? kMvLeft
-                                                     : kBad;
-                }
-            }
-            code[e] = cd;
-        }
-        __syncthreads();
-        const uint64_t t1b = __builtin_amdgcn_s_memrealtime();
-        // Multi-step codes by doubling, so that the walk below takes 4 moves per
-        // dependent LDS read: a k-step code holds the moves from a cell (2 bits
-        // each: 0 diag, 1 up, 2 left), their count and their total index step.
-        //   c2 (uint16): moves 0-3 | count 4-5 | step 6-14
-        //   c4 (uint32, in win's place -- no longer needed): moves 0-7 | count 8-10 | step 16-31
-        auto mv1 = [](uint8_t d) -> uint32_t { return d == kMvDiag ? 0u : d == kMvUp ? 1u : 2u; };
-        auto is_mv = [](uint8_t d) { return d == kMvDiag || d == kMvUp || d == kMvLeft; };
-        #pragma unroll
-        for (int kk = 0; kk < kTbPer; ++kk) {
-            const int e = tid + kk * kTbThreads;
-            // branch-free (the loads of all 16 cells issue together): a non-move
-            // reads its own code again
-            const uint8_t a = code[e];
-            const bool ma = is_mv(a);
-            const uint8_t b = code[e - (ma ? a : 0)];
-            const bool mb = ma && is_mv(b);
-            const uint32_t one = mv1(a) | (1u << 4) | ((uint32_t)a << 6);
-            const uint32_t two = mv1(a) | (mv1(b) << 2) | (2u << 4) | ((uint32_t)(a + b) << 6);
-            cc2[e] = (uint16_t)(mb ? two : ma ? one : 0u);
-        }
-        __syncthreads();
-        const uint64_t t1c = __builtin_amdgcn_s_memrealtime();
-        uint32_t *c4 = (uint32_t *)win;
-        #pragma unroll
-        for (int kk = 0; kk < kTbPer; ++kk) {
-            const int e = tid + kk * kTbThreads;
-            const uint32_t a = cc2[e];
-            const uint32_t na = (a >> 4) & 3u, da = a >> 6;
-            const uint32_t b = cc2[e - (na == 2 ? (int)da : 0)];  // (branch-free, as above)
-            const uint32_t nb = na == 2 ? (b >> 4) & 3u : 0u, db = na == 2 ? b >> 6 : 0u;
-            c4[e] = (a & 15u) | ((na == 2 ? b & 15u : 0u) << 4) | ((na + nb) << 8) | ((da + db) << 16);
-        }
-        __syncthreads();
-        const uint64_t t2 = __builtin_amdgcn_s_memrealtime();
         if (tid == 0) {
-            int idx = (rows - 1) * W + B;
-            int k = 0, q = 0;
-            for (;;) {
-                const uint32_t w = c4[idx];
-                const int n = (int)((w >> 8) & 7u);
-                if (n == 0) break;
-                ob[q++] = (uint16_t)(w & 0x7FFu);
-                k += n;
-                idx -= (int)(w >> 16);
-                if (n < 4) break;
+            int x = (int)st[0];
+            int64_t off = st[1];
+            for (int kk = 0; kk < nk; ++kk) {
+                const int k = k0 + kk;
+                wentry[2 * k] = x;
+                wentry[2 * k + 1] = off;
+                const uint32_t rec = ex[kk * W + x];
+                const uint32_t kind = rec & 3u, cnt = (rec >> 2) & 1023u, r = (rec >> 12) & 127u, xx = rec >> 19;
+                off += cnt;
+                x = (int)xx;
+                if (kind == kXCont && k + 1 < nwin) continue;
+                // the round ends in window k
+                const int64_t i0 = is - (int64_t)(k + 1) * kTbR + 1, dj = js - is + i0 - B;
+                ctl[1] = off > ops_cap ? 4 : (int64_t)kind;
+                ctl[2] = kind == kXCont ? i0 - 1 : i0 + r;
+                ctl[3] = kind == kXCont ? dj - 1 + xx : dj + r + xx;
+                ctl[4] = k + 1;
+                ctl[0] = off;
+                st[2] = 1;
+                break;
             }
-            const uint8_t d = code[idx];  // where the walk stopped: kStop, kEdge or kBad
-            const int r = idx / W, x = idx % W;
-            const int64_t steps = st[2];
-            if (d == kBad) {
-                st[3] = 2;  // not a Smith-Waterman table
-            } else if (steps + k > ops_cap) {
-                st[3] = 1;
-            } else {
-                st[0] = d == kStop ? -(i0 + r) - 1 : i0 + r;  // (kEdge: next window from here)
-                st[1] = jb + r + x;
-            }
-            st[4] = k;
+            st[0] = x;
+            st[1] = off;
         }
         __syncthreads();
-        {
-            const int k = (int)st[4];
-            const int64_t steps = st[2];
-            if (st[3] == 0)
-                for (int e = tid; 4 * e < k; e += kTbThreads) {
-                    const uint32_t w = ob[e];
-                    const int n = (int)(w >> 8);
-                    for (int m = 0; m < n; ++m) ops[steps + 4 * e + m] = (uint8_t)((w >> (2 * m)) & 3u);
-                }
-        }
-        __syncthreads();
-        if (tid == 0 && st[3] == 0) st[2] += st[4];
-        __syncthreads();
-        const uint64_t t3 = __builtin_amdgcn_s_memrealtime();
-        tl += t1 - t0;
-        tc += t2 - t1;
-        tc1 += t1b - t1;
-        tc2 += t1c - t1b;
-        tw += t3 - t2;
-        if (st[0] < 0) break;
-    }
-    __syncthreads();
-    if (tid == 0) {
-        info[0] = st[2];
-        info[1] = st[0] < 0 ? -st[0] - 1 : st[0];
-        info[2] = st[1];
-        info[3] = st[3];
-        info[4] = (int64_t)tl;  // (diagnostics: s_memrealtime ticks, 100 MHz)
-        info[5] = (int64_t)tc;
-        info[6] = (int64_t)tw;
-        info[7] = (int64_t)nwin;
-        info[8] = (int64_t)tc1;
-        info[9] = (int64_t)tc2;
+        if (st[2]) break;
     }
 }
 
-int launch_sw_traceback(const int32_t *table, int64_t pitch, int64_t n1, const uint8_t *s1, const uint8_t *s2,
-                        int32_t match, int32_t mismatch, int32_t gap, int64_t end_i, int64_t end_j,
-                        uint8_t *ops, int64_t ops_cap, int64_t *info, void *stream) {
-    hipLaunchKernelGGL(nw_sw_traceback, dim3(1), dim3(kTbThreads), 0, (hipStream_t)stream, table, pitch, n1, s1, s2, match,
-                       mismatch, gap, end_i, end_j, ops, ops_cap, info);
-    return (int)hipGetLastError();
+__global__ __launch_bounds__(256) void nw_tb_emit(const uint8_t *__restrict__ codes, int32_t B,
+                                                  const int64_t *__restrict__ wentry, const int64_t *__restrict__ ctl,
+                                                  uint8_t *__restrict__ ops) {
+    __shared__ uint32_t cdw[kTbR * kTbWMax / 4 + 1];
+    __shared__ uint8_t ob[2 * kTbR + kTbWMax + 8];
+    __shared__ int32_t nop;
+    const int k = blockIdx.x;
+    if (k >= ctl[4] || ctl[1] == 4) return;
+    const int W = 2 * B + 1, ncell = kTbR * W;  // (a multiple of 4: kTbR is)
+    const uint32_t *g = (const uint32_t *)(codes + (int64_t)k * ncell);
+    for (int e = threadIdx.x; e < ncell / 4; e += 256) cdw[e] = g[e];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int q = 0;
+        tb_walk((const uint8_t *)cdw, W, (int)wentry[2 * k], [&](uint32_t op) { ob[q++] = (uint8_t)op; });
+        nop = q;
+    }
+    __syncthreads();
+    const int64_t off = wentry[2 * k + 1];
+    for (int m = threadIdx.x; m < nop; m += 256) ops[off + m] = ob[m];
+}
+
+size_t sw_tb_scratch_bytes(int32_t maxwin, int32_t band) {
+    const size_t W = 2 * (size_t)band + 1;
+    return 64 + (size_t)maxwin * (16 + 4 * W + kTbR * W);
+}
+
+int run_sw_traceback(const int32_t *table, int64_t pitch, int64_t n1, const uint8_t *s1, const uint8_t *s2,
+                     int32_t match, int32_t mismatch, int32_t gap, int64_t end_i, int64_t end_j, uint8_t *ops,
+                     int64_t ops_cap, void *scratch, int32_t maxwin, int32_t band, int64_t *info, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    for (int q = 0; q < 10; ++q) info[q] = 0;
+    if (band < 1 || band > kTbBMax || maxwin < 1) return (int)hipErrorInvalidValue;
+    const int W = 2 * band + 1;
+    int64_t *ctl = (int64_t *)scratch;
+    int64_t *wentry = ctl + 8;
+    uint32_t *exits = (uint32_t *)(wentry + 2 * (size_t)maxwin);
+    uint8_t *codes = (uint8_t *)(exits + (size_t)maxwin * W);
+    hipError_t e = hipMemsetAsync(ctl, 0, 64, s);
+    if (e != hipSuccess) return (int)e;
+    int64_t ci = end_i, cj = end_j, h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (;;) {
+        if (ci <= 0 || cj <= 0) {  // row / column 0: the path's first cell
+            info[1] = ci;
+            info[2] = cj;
+            break;
+        }
+        const int32_t nwin = (int32_t)std::min<int64_t>((ci + kTbR) / kTbR, maxwin);
+        hipLaunchKernelGGL(nw_tb_windows, dim3((unsigned)nwin), dim3(kTbThreads), 0, s, table, pitch, n1, s1, s2,
+                           match, mismatch, gap, ci, cj, band, codes, exits);
+        hipLaunchKernelGGL(nw_tb_chain, dim3(1), dim3(1024), 0, s, exits, nwin, band, ci, cj, ops_cap, wentry, ctl);
+        hipLaunchKernelGGL(nw_tb_emit, dim3((unsigned)nwin), dim3(256), 0, s, codes, band, wentry, ctl, ops);
+        if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+        if ((e = hipMemcpyAsync(h, ctl, sizeof h, hipMemcpyDeviceToHost, s)) != hipSuccess) return (int)e;
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return (int)e;
+        info[4] += 1;     // rounds
+        info[5] += nwin;  // windows
+        info[0] = h[0];
+        if (h[1] == kXStop) {
+            info[1] = h[2];
+            info[2] = h[3];
+            break;
+        }
+        if (h[1] == kXBad || h[1] == 4) {
+            info[3] = h[1] == 4 ? 1 : 2;  // ops buffer too small / not a Smith-Waterman table
+            info[1] = h[2];
+            info[2] = h[3];
+            break;
+        }
+        ci = h[2];  // kXCont past the round's last window, or kXOut: re-centre there
+        cj = h[3];
+    }
+    return (int)hipSuccess;
 }
 
 }  // namespace nw

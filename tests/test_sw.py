@@ -126,6 +126,29 @@ def test_sw_table_and_best_vs_oracle(torch, ctx, strip, scheme, n1, n2, alpha):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("band,maxwin", [(1, 4096), (3, 1), (17, 3), (128, 2), (128, 4096)])
+@pytest.mark.parametrize("scheme", SCHEMES + [(2, -1, 0)])
+@pytest.mark.parametrize("n1,n2,alpha", [(1500, 1100, 4), (1000, 300, 20), (300, 1000, 4), (2000, 2000, 2)])
+def test_sw_traceback_windows_vs_oracle(torch, ctx, monkeypatch, band, maxwin, scheme, n1, n2, alpha):
+    """The windowed traceback (nw_sw.hip) with narrow bands and short rounds: paths
+    that leave the band and rounds that end in mid-table restart re-centred, and
+    the ops still equal the oracle's walk."""
+    monkeypatch.setenv("NW_TB_BAND", str(band))
+    monkeypatch.setenv("NW_TB_MAXWIN", str(maxwin))
+    rng = np.random.default_rng(n1 + 7 * n2 + alpha + band)
+    s1 = rng.integers(1, alpha + 1, n1).astype(np.int8)
+    s2 = rng.integers(1, alpha + 1, n2).astype(np.int8)
+    d1, d2 = torch.from_numpy(s1).cuda(), torch.from_numpy(s2).cuda()
+    tab = nwhip.Context.alloc_table(n1, n2)
+    r = ctx.fill(d1, d2, tab, scheme, mode=nwhip.MODE_SW)
+    want = oracle.sw_fill(s1, s2, scheme)
+    al, ops = ctx.sw_traceback(d1, d2, tab, (r.end_i, r.end_j), scheme)
+    wops, bi, bj = oracle.sw_traceback(s1, s2, want, (r.end_i, r.end_j), scheme)
+    np.testing.assert_array_equal(ops, wops)
+    assert (al.begin_i, al.begin_j, al.score, al.n_ops) == (bi, bj, r.score, len(wops))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("name", ["small", "t", "debug", "smid"])
 @pytest.mark.parametrize("scheme", SCHEMES)
 def test_sw_align_bdna_vs_golden(pair, name, scheme):
