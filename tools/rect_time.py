@@ -17,6 +17,7 @@ ap.add_argument("--n2", type=int, default=65536)
 ap.add_argument("--shapes", default="4:1,2:2,1:4,2:1")
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--kernel", type=int, default=0, help="0 auto, 1 strips, 2 panels")
+ap.add_argument("--flags", type=int, default=0, help="debug flags (8: no store waves, compute pace)")
 args = ap.parse_args()
 ctx = nwhip.Context(0)
 s1 = torch.from_numpy(nwhip.synth(1, args.n1)).cuda()
@@ -24,8 +25,8 @@ s2 = torch.from_numpy(nwhip.synth(2, args.n2)).cuda()
 tab = nwhip.Context.alloc_table(args.n1, args.n2)
 for sh in args.shapes.split(","):
     c, nc = (int(x) for x in sh.split(":"))
-    ctx.fill(s1, s2, tab, substrips=c, strip_waves=nc, kernel=args.kernel)
-    ts = [ctx.fill(s1, s2, tab, substrips=c, strip_waves=nc, kernel=args.kernel).kernel_ms for _ in range(args.reps)]
+    ctx.fill(s1, s2, tab, substrips=c, strip_waves=nc, kernel=args.kernel, flags=args.flags)
+    ts = [ctx.fill(s1, s2, tab, substrips=c, strip_waves=nc, kernel=args.kernel, flags=args.flags).kernel_ms for _ in range(args.reps)]
     ms = min(ts)
-    print(f"{args.n1}x{args.n2} C={c} NC={nc} ms={ms:.3f} GCUPS={args.n1 * args.n2 / (ms * 1e6):.1f} "
+    print(f"{args.n1}x{args.n2} kernel={args.kernel} flags={args.flags} C={c} NC={nc} ms={ms:.3f} GCUPS={args.n1 * args.n2 / (ms * 1e6):.1f} "
           f"all={[round(t, 2) for t in ts]}", flush=True)
