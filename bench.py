@@ -6,11 +6,14 @@ A "step" is one complete fill of the table (device-resident: sequences and
 table in HBM before the timed region; nothing copied back inside it).
 
   N = 1 : BASELINE config 3 -- 262144 x 262144 int32 table (275 GB) on one GPU.
-  N > 1 : `value` = row bands across ranks (mpi-horz contract, BASELINE config 4):
-          n1 = 524288 columns and 65536 rows per GPU (weak scaling; N = 8 is
-          512k x 512k); column bands (mpi-vert: 65536 columns per GPU x 524288
-          rows) run after it as `alt_partition`.  Launches are enqueued back to
-          back (link-word flow control, no host round trip between them);
+  N > 1 : `value` = row bands across ranks (mpi-horz halo contract, BASELINE
+          config 4): n1 = 524288 columns and 65536 rows per GPU (weak scaling;
+          N = 8 is 512k x 512k), the rows dealt to the GPUs in --band-blocks
+          blocks each (block-cyclic: every GPU is busy after N blocks instead of
+          N - 1 whole bands); the contiguous bands (mpi-horz's literal layout) and
+          column bands (mpi-vert: 65536 columns per GPU x 524288 rows) run after it
+          as `alt_partitions`.  Launches are enqueued back to back (link-word flow
+          control, no host round trip between them);
           fast-needleman-wunsch_amd/nw_bands.py, DESIGN.md "Multi-GPU".
 
 Prints ONE JSON line on rank 0 (see README / DESIGN.md for field meanings).
@@ -52,7 +55,11 @@ def parse():
                     help="N>1: the partition reported as `value`: row bands (mpi-horz, BASELINE "
                          "config 4; default) or column bands (mpi-vert)")
     ap.add_argument("--alt-partition", choices=["rows", "cols", "none"], default=None,
-                    help="N>1: the partition reported as `alt_partition` (default: the other one)")
+                    help="N>1: the alternate legs (`alt_partitions`; default: contiguous row bands "
+                         "and column bands)")
+    ap.add_argument("--band-blocks", type=int, default=0,
+                    help="N>1 row bands: blocks of rows per GPU, dealt round robin (1 = contiguous "
+                         "mpi-horz bands; 0 = auto: blocks of >= 16384 rows, 4 at the defaults)")
     ap.add_argument("--kernel", type=int, default=0,
                     help="0 auto, 1 anti-diagonal strips, 2 row-scan panels (nw_params.kernel)")
     ap.add_argument("--col-width", type=int, default=65536,

@@ -336,8 +336,25 @@ static int colband_layout(int64_t n1, int64_t n2, int32_t nb, int32_t r, const n
 
 static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *d_s2, int64_t n2,
                        const nw_params *p, const nw_band *band, const nw_colband *cb, int32_t *d_t,
-                       int64_t pitch, void *stream) {
+                       int64_t pitch, void *stream, const nw_band_cycle *cy = nullptr) {
     if (!c || !d_t || n1 < 0 || n2 < 0 || n1 >= INT32_MAX || n2 >= INT32_MAX) return NW_ERR_ARG;
+    // block-cyclic row bands: nbl blocks of n2 + 1 rows, checked as a band whose
+    // row 0 is the largest of the blocks'
+    nw_band cyb;
+    const int32_t nbl = cy ? cy->nblk : 1;
+    if (cy) {
+        if (band || cb || cy->nblk < 1 || (cy->hin_first & ~1) != 0 || (cy->hout_shift & ~1) != 0 ||
+            cy->row0_max < 0 || cy->row0_max >= INT32_MAX)
+            return NW_ERR_ARG;
+        if (!cy->halo_in && (cy->hin_first || cy->nblk > 1)) return NW_ERR_ARG;
+        if (cy->nblk > 1 && (cy->t_stride < (n2 + 1) * pitch || cy->t_stride % nw::kWave != 0)) return NW_ERR_ARG;
+        if ((int64_t)nbl * n2 >= INT32_MAX) return NW_ERR_ARG;
+        cyb.halo_in = cy->halo_in;
+        cyb.halo_out = cy->halo_out;
+        cyb.tag = cy->tag;
+        cyb.row0 = (uint32_t)cy->row0_max;
+        band = &cyb;
+    }
     if ((n1 > 0 && !d_s1) || (n2 > 0 && !d_s2)) return NW_ERR_ARG;
     if (!valid_params(p)) return NW_ERR_ARG;
     const bool sw = p->mode == NW_MODE_SW;
@@ -393,6 +410,12 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
                          band || cb ? band_kernel(p->kernel) : p->kernel);
     if (!shape_valid(s)) return NW_ERR_ARG;
     const bool panels = s.kernel == NW_KERNEL_PANELS;
+    if (cy && panels) return NW_ERR_UNSUPPORTED;  // (block cycles: the strip kernel)
+    if ((int64_t)s.nstrips * nbl > INT32_MAX / 2) return NW_ERR_ARG;
+    if (nbl > 1) {  // the launch's chain of hand-offs is nstrips * nbl tickets long
+        s.waves = std::max<int64_t>(1, std::min<int64_t>(s.waves_max, s.nstrips * nbl));
+        s.M = std::min<int64_t>(s.nstrips * nbl, s.waves + 1);
+    }
     if (cb) {  // this launch sweeps its band's strips only
         s.nstrips = strip_count;
         s.waves = std::max<int64_t>(1, std::min<int64_t>(s.waves_max, s.nstrips));
@@ -415,12 +438,12 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
         c->tagbase = 1;
     }
     // tags run up to tagbase + strip0 + nstrips (p is the GLOBAL strip index)
-    if ((uint64_t)c->tagbase + (uint64_t)strip_first + (uint64_t)s.nstrips + 2u >= 0xFFFFFFF0ull) {
+    if ((uint64_t)c->tagbase + (uint64_t)strip_first + (uint64_t)s.nstrips * nbl + 2u >= 0xFFFFFFF0ull) {
         NW_HIP_TRY(hipMemsetAsync(c->gran, 0, c->gran_cap, (hipStream_t)stream));
         c->tagbase = 1;
     }
     const int64_t qlen = nw::rowpack_len((int32_t)s.nblocks);
-    if ((st = grow((void **)&c->rowpack, &c->rowpack_cap, (size_t)qlen * 16)) != NW_OK) return st;
+    if ((st = grow((void **)&c->rowpack, &c->rowpack_cap, (size_t)qlen * 16 * nbl)) != NW_OK) return st;
     if ((st = grow((void **)&c->scratch, &c->scratch_cap, (size_t)s.waves * nw::kScratchWords * 4)) != NW_OK)
         return st;
 
@@ -441,9 +464,10 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
         if ((st = grow((void **)&c->smax, &c->smax_cap, need)) != NW_OK) return st;
         NW_HIP_TRY(hipMemsetAsync(c->smax, 0, (size_t)(s.nstrips + 8) * sizeof(int32_t), (hipStream_t)stream));
     }
-    if (nw::launch_rowpack(s1u, n1, s2u, n2, 0, perm_ok ? 1 : 0, c->meta, c->rowpack, qlen,
-                           stream) != hipSuccess)
-        return NW_ERR_HIP;
+    for (int32_t b = 0; b < nbl; ++b)  // (block b's side characters: s2 + b * n2)
+        if (nw::launch_rowpack(s1u, n1, s2u + (n2 > 0 ? (int64_t)b * n2 : 0), n2, 0, perm_ok ? 1 : 0, c->meta,
+                               (char *)c->rowpack + (int64_t)b * qlen * 16, qlen, stream) != hipSuccess)
+            return NW_ERR_HIP;
 
     nw::FillArgs a;
     std::memset(&a, 0, sizeof a);
@@ -483,6 +507,12 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
     a.timeout_ticks = (uint64_t)(p->timeout_ms > 0 ? p->timeout_ms : 20000) * 100000ull;
     a.sw = sw ? 1 : 0;
     a.smax = sw ? c->smax : nullptr;
+    a.nbl = nbl;
+    a.hin0 = cy ? cy->hin_first : 1;
+    a.hoshift = cy ? cy->hout_shift : 0;
+    a.tstride = cy ? cy->t_stride : 0;
+    a.qstride = qlen * 16;
+    a.hstride = n1 + 1;
     if ((panels ? nw::launch_panels(a, s.K, s.NC, (int)s.waves, stream)
                 : nw::launch_fill(a, s.K, s.NC, (int)s.waves, stream)) != hipSuccess)
         return NW_ERR_HIP;
@@ -490,7 +520,7 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
     if (cb && cb->feed_in &&
         nw::launch_colband_edge(cb->feed_in, d_t, pitch, n2, p->gap, start, stream) != hipSuccess)
         return NW_ERR_HIP;
-    c->tagbase += (uint32_t)(strip_first + s.nstrips) + 1u;
+    c->tagbase += (uint32_t)(strip_first + s.nstrips * nbl) + 1u;
     c->last_waves = (int)s.waves;
     c->last_strips = (int)s.nstrips;
     c->last_sub = s.K;
@@ -520,6 +550,13 @@ int nw_fill_band_async(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
                        int64_t pitch, void *stream) {
     if (!band) return NW_ERR_ARG;
     return launch_fill(c, d_s1, n1, d_s2_band, n2_band, p, band, nullptr, d_t, pitch, stream);
+}
+
+int nw_fill_band_cycle_async(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *d_s2_blocks,
+                             int64_t n2_blk, const nw_params *p, const nw_band_cycle *cy, int32_t *d_t,
+                             int64_t pitch, void *stream) {
+    if (!cy) return NW_ERR_ARG;
+    return launch_fill(c, d_s1, n1, d_s2_blocks, n2_blk, p, nullptr, nullptr, d_t, pitch, stream, cy);
 }
 
 void nw_band_layout(int64_t n2, int32_t nbands, int32_t r, int64_t *n_rows, int64_t *start) {
@@ -584,12 +621,14 @@ int nw_feed_alloc(int device, int64_t n2, uint64_t **d_feed) {
 
 int64_t nw_halo_bytes(int64_t n1) { return n1 < 0 ? 0 : (n1 + 1) * (int64_t)sizeof(uint64_t); }
 
-int nw_halo_alloc(int device, int64_t n1, uint64_t **d_halo) {
-    if (!d_halo || n1 < 0) return NW_ERR_ARG;
+int nw_halo_alloc(int device, int64_t n1, uint64_t **d_halo) { return nw_halo_alloc_regions(device, n1, 1, d_halo); }
+
+int nw_halo_alloc_regions(int device, int64_t n1, int32_t nregions, uint64_t **d_halo) {
+    if (!d_halo || n1 < 0 || nregions < 1) return NW_ERR_ARG;
     *d_halo = nullptr;
     if (device >= 0) NW_HIP_TRY(hipSetDevice(device));
     void *p = nullptr;
-    const size_t bytes = (size_t)nw_halo_bytes(n1);
+    const size_t bytes = (size_t)nw_halo_bytes(n1) * (size_t)nregions;
     hipError_t e = alloc_link_buffer(&p, bytes);
     if (e != hipSuccess) return e == hipErrorOutOfMemory ? NW_ERR_OOM : NW_ERR_HIP;
     if (hipMemset(p, 0, bytes) != hipSuccess) {

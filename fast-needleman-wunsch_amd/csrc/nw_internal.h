@@ -66,6 +66,16 @@ struct FillArgs {
     const uint64_t *feed_in;
     uint64_t *feed_out;
     uint32_t feed_tag;
+    // Block-cyclic row bands (nw_fill_band_cycle_async): the launch sweeps nbl
+    // row blocks of n2 + 1 rows one after the other (strips claimed in (block,
+    // strip) order); block b's table is table + b * tstride, its row packs
+    // rowpack + b * qstride bytes, its halo row region b of halo_in (block 0 only
+    // if hin0) and its last row goes to region b + hoshift of halo_out (if that
+    // is < nbl).  Strip slots and tags run over the whole launch.  nbl = 1,
+    // hin0 = 1, hoshift = 0: one table (every other launch).
+    int32_t nbl;
+    int32_t hin0, hoshift;
+    int64_t tstride, qstride, hstride;
 };
 bool sw_shape_ok(int substrips, int strip_waves);
 // column band r > 0: local column 0 (global column `start`) from the feed

@@ -447,10 +447,37 @@ __device__ __forceinline__ void run_iter(char *__restrict__ lds, int it, const u
     publish(3);
 }
 
-// Compute wave j of strip p.
+// One strip of a launch: its column strip pk (global: strip0 + k), its place pq
+// in the launch's chain of hand-offs (granule slot pq % M, tags tagbase + pq), and
+// the row block it belongs to -- a launch may sweep nbl row blocks of equal
+// height one after the other (block-cyclic row bands, nw_fill_band_cycle_async):
+// each block has its own table, row packs and halo regions.
+struct Blk {
+    int pk, pq;
+    int32_t *table;
+    const void *rowpack;
+    const uint64_t *halo_in;
+    uint64_t *halo_out;
+};
+__device__ __forceinline__ Blk make_blk(const FillArgs &A, int t) {
+    const int blk = A.nbl > 1 ? t / A.nstrips : 0;
+    const int k = t - blk * A.nstrips;
+    Blk B;
+    B.pk = A.strip0 + k;
+    B.pq = A.strip0 + t;
+    B.table = A.table + (int64_t)blk * A.tstride;
+    B.rowpack = (const char *)A.rowpack + (int64_t)blk * A.qstride;
+    B.halo_in = (A.halo_in != nullptr && (blk > 0 || A.hin0 != 0)) ? A.halo_in + (int64_t)blk * A.hstride : nullptr;
+    B.halo_out = (A.halo_out != nullptr && blk + A.hoshift < A.nbl) ? A.halo_out + (int64_t)(blk + A.hoshift) * A.hstride
+                                                                     : nullptr;
+    return B;
+}
+
+// Compute wave j of strip B.pk.
 template <int C, int NC, int MODE>
-__device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restrict__ lds, int p,
+__device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restrict__ lds, const Blk &B,
                                               int j, int lane) {
+    const int p = B.pk;
     typedef Lay<C, NC> L;
     constexpr bool SW = is_sw<MODE>();
     const int32_t gap = A.gap;
@@ -471,25 +498,25 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
     int32_t bnd0 = 0;
 #pragma unroll
     for (int k = 0; k < C; ++k) top[k] = (int32_t)((cl + k) * (int64_t)gw);  // SW: row 0 is 0
-    if (A.halo_in != nullptr) {
+    if (B.halo_in != nullptr) {
         const uint64_t h0 = __builtin_amdgcn_s_memrealtime();
         for (;;) {
             bool ok = true;
 #pragma unroll
             for (int k = 0; k < C; ++k) {
                 const int64_t c = min(cl + k, A.n1);
-                const uint64_t g = __hip_atomic_load(A.halo_in + c, __ATOMIC_RELAXED,
+                const uint64_t g = __hip_atomic_load(B.halo_in + c, __ATOMIC_RELAXED,
                                                      __HIP_MEMORY_SCOPE_SYSTEM);
                 top[k] = (int32_t)(uint32_t)g;
                 ok &= (uint32_t)(g >> 32) == A.halo_tag;
             }
-            const uint64_t g0 = __hip_atomic_load(A.halo_in, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            const uint64_t g0 = __hip_atomic_load(B.halo_in, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             bnd0 = (int32_t)(uint32_t)g0;
             ok &= (uint32_t)(g0 >> 32) == A.halo_tag;
             if (__all(ok)) break;
             if (ctrl_load(A.ctrl + 1) != 0u) { dead = true; break; }
             if (__builtin_amdgcn_s_memrealtime() - h0 > A.timeout_ticks) {
-                give_up(A.ctrl, 2u, 4, A.halo_in, A.halo_tag, 0);
+                give_up(A.ctrl, 2u, 4, B.halo_in, A.halo_tag, 0);
                 dead = true;
                 break;
             }
@@ -553,7 +580,7 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
     // a column band's first strip is fed by the left band (feed_in, feed_tag)
     const bool fed = p == A.strip0 && A.feed_in != nullptr;
     const bool feeds = p == A.strip0 + A.nstrips - 1 && A.feed_out != nullptr;
-    F.tag = fed ? A.feed_tag : A.tagbase + (uint32_t)p;
+    F.tag = fed ? A.feed_tag : A.tagbase + (uint32_t)B.pq;
     F.gap = gap;
     F.nslow = 0;
     F.wticks = 0;
@@ -569,14 +596,14 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
     O.gap = gap;
     const int32_t *next_done = ctr + L::kCtlWords + 2;  // iterations done by wave j+1
 
-    const uint64_t *gin = (fed ? A.feed_in : A.gran + (int64_t)((p + A.M - 1) % A.M) * A.gstride) + lane;
-    uint64_t *gout = feeds ? A.feed_out : A.gran + (int64_t)(p % A.M) * A.gstride;
-    const uint64_t tagw = (uint64_t)(feeds ? A.feed_tag : A.tagbase + (uint32_t)p + 1u) << 32;
+    const uint64_t *gin = (fed ? A.feed_in : A.gran + (int64_t)((B.pq + A.M - 1) % A.M) * A.gstride) + lane;
+    uint64_t *gout = feeds ? A.feed_out : A.gran + (int64_t)(B.pq % A.M) * A.gstride;
+    const uint64_t tagw = (uint64_t)(feeds ? A.feed_tag : A.tagbase + (uint32_t)B.pq + 1u) << 32;
     const int nblocks = A.nblocks;
     const int lastb = nblocks - 1;
     uint64_t *gscr = (uint64_t *)(A.scratch + (int64_t)blockIdx.x * kScratchWords) + lane;
 
-    const u32x4 *pkp = (const u32x4 *)A.rowpack;
+    const u32x4 *pkp = (const u32x4 *)B.rowpack;
     // Prefetch pipeline: the left neighbour's granules (feed) and the row words
     // are loaded PD iterations ahead into NB-deep register rings, so no wait for
     // a load falls inside the steps.  Buffer = iteration mod NB; all loads
@@ -684,7 +711,7 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
     ctr_store(ctr + 1, kDone);
     ctr_store(ctr + 2, kDone);
     if (A.trace != nullptr && lane == 0) {
-        uint64_t *tr = A.trace + (int64_t)(p - A.strip0) * kTraceWords;
+        uint64_t *tr = A.trace + (int64_t)(B.pq - A.strip0) * kTraceWords;
         if (j == 0) {
             tr[0] = tstart;
             tr[2] = F.nslow;
@@ -727,8 +754,9 @@ __device__ __forceinline__ void strip_max(const FillArgs &A, int p, int32_t vmax
 // HBM load one store instruction holds its wave for ~190 cycles, which is why
 // one compute wave has several store waves.
 template <int C, int NC>
-__device__ __forceinline__ void store_strip(const FillArgs &A, char *__restrict__ lds, int p,
+__device__ __forceinline__ void store_strip(const FillArgs &A, char *__restrict__ lds, const Blk &B,
                                             int j, int q, int lane) {
+    const int p = B.pk;
     typedef typename Vec<C>::T VT;
     typedef Lay<C, NC> L;
     constexpr int NR = 4 / C;                  // rows per store instruction
@@ -763,7 +791,7 @@ __device__ __forceinline__ void store_strip(const FillArgs &A, char *__restrict_
 #pragma unroll
     for (int e = 0; e < 4; ++e) cval |= (c0 + 4 * cq + e <= A.n1 ? 1u : 0u) << e;
     int32_t vmax = 0;
-    char *rowp = timing ? scr : (char *)(A.table + c0) + (int64_t)f0 * rowb;
+    char *rowp = timing ? scr : (char *)(B.table + c0) + (int64_t)f0 * rowb;
     const uint32_t voff = (uint32_t)(ro * rowb) + (uint32_t)cq * 16u;
     // col0 = 1: strip 0's first ring also stores the boundary column 0,
     // t[r][0] = t[0][0] + r*GAP (t[0][0] = 0, or the halo's column 0 for a band)
@@ -855,22 +883,22 @@ __device__ __forceinline__ void store_strip(const FillArgs &A, char *__restrict_
     // L2 back (agent release), re-read the row with sc1 loads, publish
     // system-scope granules (write-through; peer HBM over xGMI when the next
     // band lives on another GPU).  (The store wave that stored row n2 does it.)
-    if (A.halo_out != nullptr && ((nrows - 1) / BATCH) % NS == q && ctrl_load(A.ctrl + 1) == 0u) {
+    if (B.halo_out != nullptr && ((nrows - 1) / BATCH) % NS == q && ctrl_load(A.ctrl + 1) == 0u) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        const int32_t *last = A.table + A.n2 * A.pitch;
+        const int32_t *last = B.table + A.n2 * A.pitch;
 #pragma unroll
         for (int k = 0; k < C; ++k) {
             const int64_t c = c0 + (int64_t)C * lane + k;
             if (c <= A.n1) {
                 const uint32_t x = (uint32_t)__hip_atomic_load(last + c, __ATOMIC_RELAXED,
                                                                __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(A.halo_out + c, ((uint64_t)A.halo_tag << 32) | x,
+                __hip_atomic_store(B.halo_out + c, ((uint64_t)A.halo_tag << 32) | x,
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
         if (bcol && lane == 0)
-            __hip_atomic_store(A.halo_out,
+            __hip_atomic_store(B.halo_out,
                                ((uint64_t)A.halo_tag << 32) | (uint32_t)(bnd0 + (int32_t)A.n2 * A.gap),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
@@ -884,8 +912,9 @@ __device__ __forceinline__ void store_strip(const FillArgs &A, char *__restrict_
 // was computed at step f + r + a: record group (f+r+a)/4, word (f+r+a)%4).
 // Rows go in batches of kBatch dealt round robin to the kSPR store waves.
 template <int NC>
-__device__ __forceinline__ void store_strip_grp(const FillArgs &A, char *__restrict__ lds, int p,
+__device__ __forceinline__ void store_strip_grp(const FillArgs &A, char *__restrict__ lds, const Blk &B,
                                                 int j, int q, int lane) {
+    const int p = B.pk;
     typedef Lay<1, NC> L;
     constexpr int BATCH = L::kBatch;  // a multiple of 8
     constexpr int NS = L::kSPR;
@@ -931,7 +960,7 @@ __device__ __forceinline__ void store_strip_grp(const FillArgs &A, char *__restr
 #pragma unroll
         for (int k = 0; k < 4; ++k) cval |= (c0 + 32 * h + 4 * cq + k <= A.n1 ? 1u : 0u) << (4 * h + k);
     int32_t vmax = 0;
-    char *rowp = timing ? scr : (char *)(A.table + c0) + (int64_t)f0 * rowb;
+    char *rowp = timing ? scr : (char *)(B.table + c0) + (int64_t)f0 * rowb;
     const uint32_t voff = (uint32_t)(ro * rowb) + (uint32_t)cq * 16u;
     const bool bcol = A.col0 != 0 && p == 0 && j == 0 && !timing;
     int32_t bnd0 = 0;
@@ -1074,7 +1103,7 @@ __device__ __forceinline__ void store_strip_grp(const FillArgs &A, char *__restr
     ctr_store(mine, kDone);
     if (A.sw) strip_max(A, p, vmax);
     if (trace && lane == 0) {
-        uint64_t *trw = A.trace + (int64_t)(p - A.strip0) * kTraceWords;
+        uint64_t *trw = A.trace + (int64_t)(B.pq - A.strip0) * kTraceWords;
         trw[16] = tw;
         trw[17] = 0;
         trw[18] = ts;
@@ -1084,18 +1113,18 @@ __device__ __forceinline__ void store_strip_grp(const FillArgs &A, char *__restr
     // later one; with the default kSPR = 1 for C = 1 that wave also stored the
     // left half (the NW_SPR tuning override with NS > 1 is for timing builds)
     static_assert(NS == 1 || L::kSPR != 1, "");
-    if (A.halo_out != nullptr && ((nrows - 1 + kLagH) / BATCH) % NS == q && ctrl_load(A.ctrl + 1) == 0u) {
+    if (B.halo_out != nullptr && ((nrows - 1 + kLagH) / BATCH) % NS == q && ctrl_load(A.ctrl + 1) == 0u) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        const int32_t *last = A.table + A.n2 * A.pitch;
+        const int32_t *last = B.table + A.n2 * A.pitch;
         const int64_t c = c0 + lane;
         if (c <= A.n1) {
             const uint32_t x = (uint32_t)__hip_atomic_load(last + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(A.halo_out + c, ((uint64_t)A.halo_tag << 32) | x, __ATOMIC_RELAXED,
+            __hip_atomic_store(B.halo_out + c, ((uint64_t)A.halo_tag << 32) | x, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
         }
         if (bcol && lane == 0)
-            __hip_atomic_store(A.halo_out,
+            __hip_atomic_store(B.halo_out,
                                ((uint64_t)A.halo_tag << 32) | (uint32_t)(bnd0 + (int32_t)A.n2 * A.gap),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
@@ -1126,8 +1155,8 @@ __global__ __launch_bounds__((64 * Lay<C, NC>::kWaves)) void nw_fill_strips(Fill
         }
         __syncthreads();
         const int t = __builtin_amdgcn_readfirstlane(ctl[L::kStripWord]);
-        if (t >= A.nstrips) break;
-        const int p = A.strip0 + t;  // global strip index
+        if (t >= A.nstrips * A.nbl) break;
+        const Blk B = make_blk(A, t);
         if (wave < NC) {
             // table form when the launch allows it (scores fit int8) and s1 has
             // at most kMaxPerm distinct characters (nw_charmap), else compares
@@ -1136,26 +1165,26 @@ __global__ __launch_bounds__((64 * Lay<C, NC>::kWaves)) void nw_fill_strips(Fill
             if constexpr (sw_shape(C, NC) && !UNIT) {  // (SW launches use the generic kernel)
                 if (A.sw) {
                     if (A.perm != 0 && np <= kMaxPerm)
-                        compute_strip<C, NC, SUB_PERM_SW>(A, lds, p, wave, lane);
+                        compute_strip<C, NC, SUB_PERM_SW>(A, lds, B, wave, lane);
                     else
-                        compute_strip<C, NC, SUB_GEN_SW>(A, lds, p, wave, lane);
+                        compute_strip<C, NC, SUB_GEN_SW>(A, lds, B, wave, lane);
                     sw_done = true;
                 }
             }
             if (sw_done) {
             } else if (A.perm != 0 && np <= kMaxPerm) {
-                compute_strip<C, NC, SUB_PERM>(A, lds, p, wave, lane);
+                compute_strip<C, NC, SUB_PERM>(A, lds, B, wave, lane);
             } else if (UNIT) {
-                compute_strip<C, NC, SUB_UNIT>(A, lds, p, wave, lane);
+                compute_strip<C, NC, SUB_UNIT>(A, lds, B, wave, lane);
             } else {
-                compute_strip<C, NC, SUB_GEN>(A, lds, p, wave, lane);
+                compute_strip<C, NC, SUB_GEN>(A, lds, B, wave, lane);
             }
         } else {
             const int b = wave - NC;
             if constexpr (L::kGrp)
-                store_strip_grp<NC>(A, lds, p, b % NC, b / NC, lane);
+                store_strip_grp<NC>(A, lds, B, b % NC, b / NC, lane);
             else
-                store_strip<C, NC>(A, lds, p, b % NC, b / NC, lane);
+                store_strip<C, NC>(A, lds, B, b % NC, b / NC, lane);
         }
         __syncthreads();  // the rings and counters are reused by the next strip
     }

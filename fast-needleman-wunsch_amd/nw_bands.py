@@ -123,6 +123,99 @@ class LocalBands:
             c.close()
 
 
+def cycle_layout(n2: int, nranks: int, nblk: int):
+    """Block-cyclic row bands (nw_fill_band_cycle_async): the n2 rows below row 0
+    cut into nranks * nblk blocks of h rows, global block g = k * nranks + r being
+    rank r's block k, its row 0 = global row g * h (the previous block's last row).
+    Returns h; n2 must be a multiple of nranks * nblk."""
+    nb = nranks * nblk
+    if nranks < 1 or nblk < 1 or n2 < nb or n2 % nb:
+        raise ValueError(f"block-cyclic bands need n2 = {n2} to be a positive multiple of {nb} blocks")
+    return n2 // nb
+
+
+def cycle_side_chars(s2, h: int, nranks: int, nblk: int, r: int):
+    """Rank r's side characters, block k's h of them at [k*h, (k+1)*h): global
+    rows g*h + 1 .. (g+1)*h use s2[g*h : (g+1)*h], g = k * nranks + r."""
+    return np.concatenate([s2[(k * nranks + r) * h:(k * nranks + r + 1) * h] for k in range(nblk)])
+
+
+class LocalCycleBands:
+    """Block-cyclic row bands of one (n2+1) x (n1+1) table on ONE device, P ranks
+    (contexts, 1/P of the resident workers each) of nblk blocks, halo regions
+    r -> r+1 (and P-1 -> 0 for the next block) through device buffers -- the
+    single-GPU parity vehicle of the multi-GPU block-cyclic partition.
+
+    P = 1: the rank's nblk blocks in ONE launch (nw_fill_band_cycle_async chains
+    them through its own halo buffer: the multi-block kernel path).  P > 1: one
+    launch per block, enqueued in global block order on its rank's stream (the
+    same kernel and halo regions; per-rank launches of all blocks need the P
+    launches co-resident, which one process cannot promise: HIP maps its streams
+    onto a few hardware queues, and rank 0 -- waiting on rank P-1 -- must not sit
+    in front of it in one.  One process per GPU has no such limit: bench.py
+    --share-gpu under torch.distributed.run rehearses that)."""
+
+    def __init__(self, n1: int, n2: int, nranks: int, nblk: int, device: int = 0, substrips: int = 0,
+                 strip_waves: int = 0):
+        import torch
+        self.n1, self.n2, self.P, self.m, self.device = n1, n2, nranks, nblk, device
+        self.h = cycle_layout(n2, nranks, nblk)
+        self.substrips, self.strip_waves = band_shape(n1, self.h, substrips, strip_waves)
+        self.tables = [nwhip.Context.alloc_cycle_tables(n1, self.h, nblk) for _ in range(nranks)]
+        self.halos = [nwhip.Halo(n1, device, regions=nblk) for _ in range(nranks)]
+        self.ctxs = [nwhip.Context(device) for _ in range(nranks)]
+        self.streams = [torch.cuda.Stream(device) for _ in range(nranks)]
+        self.waves = max(1, resident_waves(device, self.substrips, self.strip_waves) // nranks)
+        self.region = 8 * (n1 + 1)  # bytes per halo region (nw_halo_bytes)
+        self.tag = 0
+
+    def block(self, g: int):
+        """(table of global block g, global row of its row 0)."""
+        return self.tables[g % self.P][g // self.P], g * self.h
+
+    def fill(self, d_s1, s2: np.ndarray, scheme=(1, 0, -1), flags: int = 0, timeout_ms: int = 0) -> int:
+        """Fill every block; returns the final score t[n2][n1] (the last block's last cell)."""
+        import torch
+        assert int(d_s1.numel()) == self.n1 and s2.size == self.n2
+        self.tag += 1
+        P, m, h = self.P, self.m, self.h
+        cur = torch.cuda.current_stream(self.device)
+        sides = [torch.from_numpy(cycle_side_chars(s2, h, P, m, r)).cuda(self.device) for r in range(P)]
+        for st in self.streams:
+            st.wait_stream(cur)
+        kw = dict(tag=self.tag, scheme=scheme, waves=self.waves, flags=flags, substrips=self.substrips,
+                  strip_waves=self.strip_waves, timeout_ms=timeout_ms)
+        if P == 1:
+            self.ctxs[0].fill_band_cycle(d_s1, sides[0], h, self.tables[0], halo_in=self.halos[0].ptr,
+                                         halo_out=self.halos[0].ptr, hin_first=False, hout_shift=1,
+                                         row0_max=(m - 1) * h, stream=self.streams[0], **kw)
+        else:
+            for g in range(P * m):
+                r, k = g % P, g // P
+                nxt = (r + 1) % P  # block g + 1 lives on rank nxt, as its block k (or k + 1 after the wrap)
+                kn = k + 1 if r == P - 1 else k
+                self.ctxs[r].fill_band_cycle(
+                    d_s1, sides[r][k * h:(k + 1) * h], h, self.tables[r][k:k + 1],
+                    halo_in=self.halos[r].ptr + k * self.region, hin_first=g > 0,
+                    halo_out=self.halos[nxt].ptr + kn * self.region if g + 1 < P * m else None,
+                    hout_shift=0, row0_max=g * h, stream=self.streams[r], **kw)
+        for r, st in enumerate(self.streams):
+            s = self.ctxs[r].status(st)
+            if s != nwhip.NW_OK:
+                diag = [c.debug_ctrl() for c in self.ctxs]
+                raise nwhip.NwError(s, f"cyclic bands, rank {r} (control words per rank: {diag})")
+            cur.wait_stream(st)
+        torch.cuda.synchronize(self.device)
+        del sides
+        return int(self.tables[P - 1][m - 1, h, self.n1].item())
+
+    def close(self):
+        for hb in self.halos:
+            hb.free()
+        for c in self.ctxs:
+            c.close()
+
+
 # Per-row pace (ns) of a strip in a store-saturated sweep, per strip shape (C, NC):
 # tools/rect_time.py on 65536 x 524288 (one pass of 256 strips): T = pace *
 # (n2 + 255 * 64 * NC) gives (4,1) 35.7 ms -> 66.1, (2,2) 37.0 -> 66.4, (1,4) 29.7 -> 50.3
@@ -224,20 +317,25 @@ def _golden(n1: int, n2: int, scheme):
     return g.get(key)
 
 
-def _sweep(args, partition: str, rank: int, world: int, dev: int, scheme) -> dict:
+def _sweep(args, partition: str, rank: int, world: int, dev: int, scheme, blocks: int = 1) -> dict:
     """One multi-rank band sweep: `warmup` + `steps` fills enqueued back to back on
     this rank's stream, halo / feed buffers alternating by launch parity, the
     producer's stream waiting on the consumer's "done with launch k" link word
     (nw_link_*) before it rewrites that launch's buffer -- no host round trip
-    between launches.  Returns this rank's measurements (wall time of the timed
-    launches between a barrier + synchronize on both sides)."""
+    between launches.  partition: "rows" (mpi-horz: contiguous row bands, or
+    block-cyclic ones with args.band_blocks > 1 blocks per rank), "cols" (mpi-vert).
+    Returns this rank's measurements (wall time of the timed launches between a
+    barrier + synchronize on both sides)."""
     import torch
     import torch.distributed as dist
 
     cols = partition == "cols"
     kernel = getattr(args, "kernel", 0)
+    m = max(1, blocks) if not cols else 1
+    cyc = m > 1
     ctx = nwhip.Context(dev)
     stream = torch.cuda.current_stream()
+    h = 0
     if cols:
         # column bands (mpi-vert): rank r owns ~col_width columns of every row
         n1, n2 = world * args.col_width, args.col_rows
@@ -248,6 +346,16 @@ def _sweep(args, partition: str, rank: int, world: int, dev: int, scheme) -> dic
         table = nwhip.Context.alloc_table(ncols - 1, n2)
         links_in = [nwhip.Feed(n2, dev) for _ in range(2)] if rank > 0 else None
         rows = n2 + 1
+    elif cyc:
+        # block-cyclic row bands: rank r owns blocks g = k * world + r of h rows
+        n1, n2 = args.band_cols, world * args.band_rows
+        h = cycle_layout(n2, world, m)
+        s1 = torch.from_numpy(nwhip.synth(1, n1)).cuda()
+        s2 = torch.from_numpy(cycle_side_chars(nwhip.synth(2, n2), h, world, m, rank)).cuda()
+        table = nwhip.Context.alloc_cycle_tables(n1, h, m)
+        links_in = [nwhip.Halo(n1, dev, regions=m) for _ in range(2)]
+        sub, nc = band_shape(n1, h, args.substrips, args.strip_waves)
+        rows, start, ncols = h + 1, ((m - 1) * world + rank) * h, n1 + 1
     else:
         # row bands (mpi-horz, BASELINE config 4): rank r owns band_rows rows
         n1 = args.band_cols
@@ -260,15 +368,18 @@ def _sweep(args, partition: str, rank: int, world: int, dev: int, scheme) -> dic
         links_in = [nwhip.Halo(n1, dev) for _ in range(2)] if rank > 0 else None
         sub, nc = band_shape(n1, rows - 1, args.substrips, args.strip_waves, kernel)
         ncols = n1 + 1
-    # rank r exports its two incoming buffers and (r < world-1) the link word its
-    # consumer r+1 signals into; rank r maps r+1's buffers and r-1's word
-    link_word = nwhip.Link(dev) if rank + 1 < world else None
+    # the chain: rank r feeds r+1 (and, block-cyclic, the last rank feeds rank 0's
+    # next block).  Rank r exports its two incoming buffers and the link word its
+    # consumer signals into; it maps its consumer's buffers and its producer's word.
+    consumer = (rank + 1) % world if (rank + 1 < world or cyc) else None
+    producer = (rank - 1) % world if (rank > 0 or cyc) else None
+    link_word = nwhip.Link(dev) if consumer is not None else None
     mine = ([nwhip.ipc_get_handle(b.ptr) for b in links_in] if links_in else None,
             nwhip.ipc_get_handle(link_word.ptr) if link_word else None)
     handles = [None] * world
     dist.all_gather_object(handles, mine)
-    out_bufs = [nwhip.ipc_open_handle(h) for h in handles[rank + 1][0]] if rank + 1 < world else None
-    prod_word = nwhip.ipc_open_handle(handles[rank - 1][1]) if rank > 0 else None
+    out_bufs = [nwhip.ipc_open_handle(x) for x in handles[consumer][0]] if consumer is not None else None
+    prod_word = nwhip.ipc_open_handle(handles[producer][1]) if producer is not None else None
     waves = args.waves
     if args.share_gpu and waves == 0:
         waves = max(1, resident_waves(dev, sub, nc, kernel) // world)
@@ -285,6 +396,9 @@ def _sweep(args, partition: str, rank: int, world: int, dev: int, scheme) -> dic
         if cols:
             ctx.fill_colband(s1, s2, table, world, rank, feed_in=links_in[b].ptr if links_in else None,
                              feed_out=out_bufs[b] if out_bufs else None, **kw)
+        elif cyc:
+            ctx.fill_band_cycle(s1, s2, h, table, halo_in=links_in[b].ptr, halo_out=out_bufs[b],
+                                hin_first=rank > 0, hout_shift=int(rank == world - 1), row0_max=start, **kw)
         else:
             ctx.fill_band(s1, s2, table, halo_in=links_in[b].ptr if links_in else None,
                           halo_out=out_bufs[b] if out_bufs else None, row0=start, **kw)
@@ -309,7 +423,8 @@ def _sweep(args, partition: str, rank: int, world: int, dev: int, scheme) -> dic
     status = ctx.status()
     link_status = link_word.status() if link_word else 0
     kms = float(np.mean([a.elapsed_time(b) for a, b in evs])) if evs else 0.0
-    score = int(table[rows - 1, ncols - 1].item()) if rank == world - 1 else None
+    last = table[m - 1] if cyc else table
+    score = int(last[rows - 1, ncols - 1].item()) if rank == world - 1 else None
     dist.barrier()
     if out_bufs:
         for x in out_bufs:
@@ -320,18 +435,61 @@ def _sweep(args, partition: str, rank: int, world: int, dev: int, scheme) -> dic
     for x in (links_in or []) + ([link_word] if link_word else []):
         x.free()
     ctx.close()
-    del table
+    del table, last
     torch.cuda.empty_cache()
     return {"wall": wall, "status": status, "link_status": link_status, "kms": kms, "score": score,
-            "n1": n1, "n2": n2, "shape": [sub, nc], "kernel": kernel, "rows": rows, "start": start}
+            "n1": n1, "n2": n2, "shape": [sub, nc], "kernel": kernel, "rows": rows, "start": start,
+            "blocks": m, "block_rows": h}
+
+
+# Rows per block below which a block-cyclic launch starves its workers: strips are
+# claimed in (block, strip) order and a block's strips start one hop (64 * NC rows
+# of the anti-diagonal skew) apart, so a block keeps only h / hop of them busy --
+# all 256+ workers need h >= 256 * 64 rows with the (4, 1) strips of a wide block.
+CYCLE_MIN_BLOCK_ROWS = 16384
+
+
+def auto_blocks(args) -> int:
+    """Blocks per rank of the row-band leg: --band-blocks, or (0 = auto) as many as
+    keep every block at least CYCLE_MIN_BLOCK_ROWS rows (1 = contiguous bands);
+    the panel kernel has no block-cyclic launch (1)."""
+    if getattr(args, "kernel", 0) == nwhip.KERNEL_PANELS:
+        return 1
+    m = getattr(args, "band_blocks", 0)
+    if m <= 0:
+        m = max(1, args.band_rows // CYCLE_MIN_BLOCK_ROWS)
+        while m > 1 and args.band_rows % m:
+            m -= 1
+    return m
+
+
+def legs_for(args) -> list:
+    """[(name, partition, blocks per rank)] of a multi-GPU bench: the main one
+    first (its value is the line's), then the alternates (--alt-partition)."""
+    main = getattr(args, "partition", "rows")
+    m = auto_blocks(args)
+    rows_main = ("rows_cyclic", "rows", m) if m > 1 else ("rows_contiguous", "rows", 1)
+    legs = [rows_main] if main == "rows" else [("cols", "cols", 1)]
+    alt = getattr(args, "alt_partition", None)
+    if alt == "none":
+        return legs
+    if main == "rows":
+        if m > 1 and alt in (None, "rows"):
+            legs.append(("rows_contiguous", "rows", 1))
+        if alt in (None, "cols"):
+            legs.append(("cols", "cols", 1))
+    elif alt in (None, "rows"):
+        legs.append(rows_main if m > 1 else ("rows_contiguous", "rows", 1))
+    return legs
 
 
 def run_bands(args) -> dict | None:
     """bench.py --gpus N (N > 1) under torch.distributed.run: one rank per GPU.
-    `value` = row bands (BASELINE config 4, mpi-horz): rank r fills band r of an
-    n1 x (N * band_rows) table (weak scaling: per-GPU band fixed; at N = 8 with the
-    defaults this is 512k x 512k).  The other partition (column bands, mpi-vert:
-    N * col_width columns x col_rows rows) runs after it as `alt_partition` unless
+    `value` = row bands (BASELINE config 4: an n1 x (N * band_rows) table, weak
+    scaling, 512k x 512k at N = 8 with the defaults), by default block-cyclic
+    (--band-blocks blocks of rows per rank, mpi-horz's halo contract per block);
+    the contiguous mpi-horz bands (--band-blocks 1) and the column bands (mpi-vert,
+    N * col_width columns x col_rows rows) run after it as `alt_partitions` unless
     --alt-partition none.  Prints and returns the JSON line on rank 0."""
     import torch
     import torch.distributed as dist
@@ -346,28 +504,31 @@ def run_bands(args) -> dict | None:
     if not dist.is_initialized():
         dist.init_process_group("gloo", rank=rank, world_size=world)
     scheme = tuple(int(x) for x in args.scheme.split(","))
-    main = getattr(args, "partition", "rows")
-    alt = getattr(args, "alt_partition", None)
-    if alt is None:
-        alt = "cols" if main == "rows" else "rows"
     legs = {}
-    for part in [main] + ([alt] if alt not in ("none", main) else []):
-        m = _sweep(args, part, rank, world, dev, scheme)
+    plan_ = legs_for(args)
+    for name, part, m in plan_:
+        r = _sweep(args, part, rank, world, dev, scheme, m)
         allm = [None] * world
-        dist.all_gather_object(allm, m)
-        legs[part] = allm
+        dist.all_gather_object(allm, r)
+        legs[name] = (part, allm)
     if rank != 0:
         return None
-    out = _line(args, world, scheme, main, legs[main])
-    if alt in legs:
-        a = _line(args, world, scheme, alt, legs[alt])
-        out["alt_partition"] = {k: a[k] for k in ("value", "ms_per_step", "config", "score", "score_golden",
-                                                  "score_ok", "roofline")}
+    name0 = plan_[0][0]
+    out = _line(args, world, scheme, *legs[name0])
+    alts = {}
+    for name, _, _ in plan_[1:]:
+        a = _line(args, world, scheme, *legs[name])
+        alts[name] = {k: a[k] for k in ("value", "ms_per_step", "config", "score", "score_golden", "score_ok",
+                                        "roofline")}
+    if alts:
+        out["alt_partitions"] = alts
+        if name0 == "rows_cyclic" and "rows_contiguous" in alts:  # the same table, two partitions
+            out["rows_legs_agree"] = alts["rows_contiguous"]["score"] == out["score"]
     if cpu_baseline_fn is not None and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_fn(args.cpu_n, scheme)
     print(json.dumps(out), flush=True)
-    bad = [(p, [m["status"] for m in legs[p]], [m["link_status"] for m in legs[p]]) for p in legs
-           if any(m["status"] != 0 or m["link_status"] != 0 for m in legs[p])]
+    bad = [(p, [m["status"] for m in ms], [m["link_status"] for m in ms]) for p, (_, ms) in legs.items()
+           if any(m["status"] != 0 or m["link_status"] != 0 for m in ms)]
     if bad:
         raise RuntimeError(f"band status per rank (fill, link): {bad}")
     return out
@@ -399,9 +560,18 @@ def _line(args, world: int, scheme, part: str, ms: list) -> dict:
         cfg = {"workload": f"nw_fill_colbands_{n2}x{n1}", "col_width": args.col_width,
                "parallelism": f"column bands x{world} (mpi-vert)",
                "halo": "in-kernel xGMI peer stores of the band's right column, 16 rows at a time", **common}
+    elif m0["blocks"] > 1:
+        cfg = {"workload": f"nw_fill_rowbands_{n2}x{n1}", "band_rows": args.band_rows,
+               "blocks_per_gpu": m0["blocks"], "block_rows": m0["block_rows"],
+               "parallelism": f"row bands x{world}, block-cyclic: {m0['blocks']} blocks of {m0['block_rows']} rows "
+                              f"per GPU, block g on GPU g mod {world} (mpi-horz halo contract per block, "
+                              "BASELINE config 4)",
+               "halo": "in-kernel xGMI peer stores of each block's last row into the next GPU's halo region, "
+                       "as each strip finishes (the last GPU feeds GPU 0's next block)",
+               **common}
     else:
         cfg = {"workload": f"nw_fill_rowbands_{n2}x{n1}", "band_rows": args.band_rows,
-               "parallelism": f"row bands x{world} (mpi-horz, BASELINE config 4)",
+               "parallelism": f"row bands x{world}, contiguous (mpi-horz, BASELINE config 4)",
                "halo": "in-kernel xGMI peer stores of the band's last row, as each strip/panel finishes",
                **common}
     return {

@@ -35,7 +35,8 @@ EXPORTS = ["nw_params_default", "nw_strerror", "nw_version", "nw_fill", "nw_tabl
            "nw_halo_free", "nw_fill_emb", "nw_sw_align", "nw_sw_traceback", "nw_tuned_shape", "nw_auto_shape", "nw_debug_ctrl", "nw_debug_set_trace",
            "nw_debug_trace_words", "nw_colband_layout", "nw_feed_bytes", "nw_feed_alloc",
            "nw_fill_colband_async", "nw_link_alloc", "nw_link_wait_async", "nw_link_signal_async",
-           "nw_link_status", "nw_host_warmup", "nw_host_release"]
+           "nw_link_status", "nw_host_warmup", "nw_host_release", "nw_halo_alloc_regions",
+           "nw_fill_band_cycle_async"]
 IPC_HANDLE_BYTES = 64
 
 
@@ -67,6 +68,13 @@ class NwBand(ctypes.Structure):
     """nw_band (include/nw_hip.h): halo granule buffers of one row band."""
     _fields_ = [("halo_in", ctypes.c_void_p), ("halo_out", ctypes.c_void_p),
                 ("tag", ctypes.c_uint32), ("row0", ctypes.c_uint32)]
+
+
+class NwBandCycle(ctypes.Structure):
+    """nw_band_cycle (include/nw_hip.h): one rank's blocks of block-cyclic row bands."""
+    _fields_ = [("halo_in", ctypes.c_void_p), ("halo_out", ctypes.c_void_p), ("nblk", ctypes.c_int32),
+                ("hin_first", ctypes.c_int32), ("hout_shift", ctypes.c_int32), ("tag", ctypes.c_uint32),
+                ("row0_max", ctypes.c_int64), ("t_stride", ctypes.c_int64)]
 
 
 class NwColBand(ctypes.Structure):
@@ -157,6 +165,10 @@ def lib() -> ctypes.CDLL:
     L.nw_ipc_close_handle.argtypes = [ctypes.c_void_p]
     L.nw_halo_alloc.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p)]
     L.nw_halo_free.argtypes = [ctypes.c_void_p]
+    L.nw_halo_alloc_regions.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p)]
+    L.nw_fill_band_cycle_async.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                           ctypes.c_int64, ctypes.POINTER(NwParams), ctypes.POINTER(NwBandCycle),
+                                           ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
     L.nw_tuned_shape.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(ctypes.c_int32),
                                  ctypes.POINTER(ctypes.c_int32)]
     L.nw_tuned_shape.restype = None
@@ -379,14 +391,15 @@ def halo_bytes(n1: int) -> int:
 
 
 class Halo:
-    """A zeroed halo granule buffer (n1+1 x {tag, value}) in its own allocation."""
+    """A zeroed halo granule buffer (regions x (n1+1) {tag, value}) in its own
+    allocation (one region per row block for block-cyclic bands)."""
 
-    def __init__(self, n1: int, device: int = -1):
+    def __init__(self, n1: int, device: int = -1, regions: int = 1):
         ptr = ctypes.c_void_p()
-        st = lib().nw_halo_alloc(device, n1, ctypes.byref(ptr))
+        st = lib().nw_halo_alloc_regions(device, n1, regions, ctypes.byref(ptr))
         if st != NW_OK:
-            raise NwError(st, "nw_halo_alloc")
-        self.ptr, self.n1 = int(ptr.value), n1
+            raise NwError(st, "nw_halo_alloc_regions")
+        self.ptr, self.n1, self.regions = int(ptr.value), n1, regions
 
     def free(self):
         if self.ptr:
@@ -513,6 +526,17 @@ class Context:
         shift = (-(flat.data_ptr() // 4) + off) % 64  # torch allocations are 512-B aligned
         return flat[shift:shift + rows * pitch].view(rows, pitch)
 
+    @staticmethod
+    def alloc_cycle_tables(n1: int, n2_blk: int, nblk: int, device="cuda"):
+        """(nblk, table_rows(n2_blk), table_pitch(n1)) int32 view: nblk block tables
+        laid out like alloc_table's, back to back (t_stride = rows * pitch)."""
+        import torch
+        rows, pitch = table_rows(n2_blk), table_pitch(n1)
+        off = table_offset() if n1 >= 1 else 0
+        flat = torch.empty(nblk * rows * pitch + 64, dtype=torch.int32, device=device)
+        shift = (-(flat.data_ptr() // 4) + off) % 64
+        return flat[shift:shift + nblk * rows * pitch].view(nblk, rows, pitch)
+
     def fill(self, d_s1, d_s2, table, scheme=(1, 0, -1), waves: int = 0, stream=None,
              sync: bool = True, flags: int = 0, substrips: int = 0, strip_waves: int = 0,
              timeout_ms: int = 0, mode: int = MODE_NW, kernel: int = KERNEL_AUTO):
@@ -539,6 +563,33 @@ class Context:
         if st != NW_OK:
             raise NwError(st, "nw_fill_device_async")
         return None
+
+    def fill_band_cycle(self, d_s1, d_s2_blocks, n2_blk: int, tables, halo_in=None, halo_out=None,
+                        hin_first: bool = False, hout_shift: int = 0, tag: int = 1, row0_max: int = 0,
+                        scheme=(1, 0, -1), waves: int = 0, stream=None, flags: int = 0, substrips: int = 0,
+                        strip_waves: int = 0, timeout_ms: int = 0, kernel: int = KERNEL_AUTO) -> None:
+        """Launch one rank's blocks of block-cyclic row bands (asynchronous,
+        nw_fill_band_cycle_async).  d_s2_blocks: the blocks' side characters, block
+        k at [k * n2_blk, (k+1) * n2_blk); tables: alloc_cycle_tables(n1, n2_blk,
+        nblk) (block k = tables[k]); halo_in / halo_out: raw device addresses of
+        nblk-region halo buffers (Halo(..., regions=nblk).ptr or peer memory)."""
+        import torch
+        n1 = int(d_s1.numel())
+        nblk = int(tables.shape[0])
+        assert tables.dtype == torch.int32 and tables.is_contiguous() and tables.dim() == 3
+        assert int(d_s2_blocks.numel()) == nblk * n2_blk
+        assert tables.shape[1] >= table_rows(n2_blk) and tables.shape[2] >= n1 + 1 and tables.shape[2] % 64 == 0
+        if stream is None:
+            stream = torch.cuda.current_stream(tables.device)
+        cy = NwBandCycle(halo_in, halo_out, nblk, int(bool(hin_first)), int(hout_shift), int(tag), int(row0_max),
+                         int(tables.stride(0)))
+        p = params(scheme, waves, self.device, flags, substrips, strip_waves, timeout_ms, kernel=kernel)
+        st = lib().nw_fill_band_cycle_async(self._h, ctypes.c_void_p(d_s1.data_ptr() if n1 else 0), n1,
+                                            ctypes.c_void_p(d_s2_blocks.data_ptr() if n2_blk else 0), n2_blk,
+                                            ctypes.byref(p), ctypes.byref(cy), ctypes.c_void_p(tables.data_ptr()),
+                                            tables.shape[2], ctypes.c_void_p(stream.cuda_stream))
+        if st != NW_OK:
+            raise NwError(st, "nw_fill_band_cycle_async")
 
     def fill_band(self, d_s1, d_s2_band, table, halo_in=None, halo_out=None, tag: int = 1,
                   scheme=(1, 0, -1), waves: int = 0, stream=None, flags: int = 0,

@@ -290,6 +290,40 @@ int nw_fill_band_async(nw_ctx *ctx, const int8_t *d_s1, int64_t n1, const int8_t
                        int64_t n2_band, const nw_params *p, const nw_band *band, int32_t *d_t,
                        int64_t pitch, void *stream);
 
+/* Block-cyclic row bands (the config-4 row-band case, pipelined) --------------
+ * Same contract as nw_fill_band_async (mpi-horz.cpp:4-99: a block's row 0 is the
+ * previous block's last row, streamed strip by strip), but the table's rows are
+ * cut into P * nblk blocks of n2_blk rows dealt round robin to the P ranks --
+ * global block g = k * P + r is rank r's block k -- so that every rank is busy
+ * after P blocks instead of waiting for P - 1 whole bands.  One launch fills all
+ * of a rank's blocks, strips claimed in (block, strip) order:
+ *   * block k's table is d_t + k * t_stride (each laid out like a band: n2_blk + 1
+ *     rows, row 0 = the halo row), its side characters d_s2_blocks + k * n2_blk;
+ *   * its halo row comes from region k of halo_in (regions of nw_halo_bytes(n1),
+ *     nw_halo_alloc_regions) -- block 0 only if hin_first (rank 0: block 0's
+ *     row 0 is the boundary);
+ *   * its last row goes to region k + hout_shift of halo_out (the next rank's
+ *     halo_in; hout_shift = 1 on the last rank, whose block k feeds rank 0's
+ *     block k + 1; regions >= nblk are not written).  With P = 1, halo_out =
+ *     halo_in and hout_shift = 1 chain a rank's blocks through its own buffer.
+ * Strip kernel only (NW_ERR_UNSUPPORTED for panels). */
+typedef struct nw_band_cycle {
+    const uint64_t *halo_in;
+    uint64_t *halo_out;
+    int32_t nblk;
+    int32_t hin_first;
+    int32_t hout_shift;
+    uint32_t tag;             /* as nw_band.tag                                       */
+    int64_t row0_max;         /* global row of the last block's row 0 (range check)   */
+    int64_t t_stride;         /* int32 elements between blocks' tables (>= (n2_blk+1) * pitch,
+                                 a multiple of 64)                                     */
+} nw_band_cycle;
+
+int nw_halo_alloc_regions(int device, int64_t n1, int32_t nregions, uint64_t **d_halo);
+int nw_fill_band_cycle_async(nw_ctx *ctx, const int8_t *d_s1, int64_t n1, const int8_t *d_s2_blocks,
+                             int64_t n2_blk, const nw_params *p, const nw_band_cycle *cy, int32_t *d_t,
+                             int64_t pitch, void *stream);
+
 /* Column bands (multi-GPU, n1 >> n2) ------------------------------------------
  * The reference's twin is src/mpi/mpi-vert.cpp:4-109 (+ mpi-vert-driver.cpp:35-38):
  * rank r fills a contiguous band of columns whose column 0 is rank r-1's last

@@ -165,20 +165,21 @@ def test_local_bands_32k_score(torch_gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kernel", [1, 2])
-def test_two_process_bands_shared_gpu(torch_gpu, kernel):
+@pytest.mark.parametrize("kernel,blocks", [(1, 1), (2, 1), (1, 4)])
+def test_two_process_bands_shared_gpu(torch_gpu, kernel, blocks):
     """The bench's multi-process path end to end on one GPU: 2 ranks (torch.distributed.run,
     gloo control plane), IPC-mapped halo / feed buffers alternating by launch parity,
     link-word flow control between back-to-back launches, in-kernel halo stores; the
-    row-band leg (`value`) and the column-band leg (`alt_partition`) both against the
-    oracle, for both kernel families."""
-    n1, rows = 4096 + 17, 700
+    row-band leg (`value`: contiguous, or block-cyclic with 4 blocks per rank, where
+    the last rank also feeds rank 0) and the alternate legs (`alt_partitions`: the
+    contiguous rows, the column bands) all against the oracle, both kernel families."""
+    n1, rows = 4096 + 17, 704
     width, crows = 1500, 1300
     env = dict(os.environ, PYTHONPATH=PKG)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "2",
-           "--share-gpu", "--partition", "rows", "--alt-partition", "cols", "--band-rows", str(rows),
+           "--share-gpu", "--partition", "rows", "--band-rows", str(rows), "--band-blocks", str(blocks),
            "--band-cols", str(n1), "--col-width", str(width), "--col-rows", str(crows),
            "--kernel", str(kernel), "--no-cpu-baseline"]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
@@ -188,9 +189,12 @@ def test_two_process_bands_shared_gpu(torch_gpu, kernel):
     n2 = 2 * rows
     want = oracle.score(nwhip.synth(1, n1), nwhip.synth(2, n2))
     assert res["score"] == want and res["n_gpus"] == 2 and res["config"]["n2"] == n2
-    alt = res["alt_partition"]
-    assert alt["score"] == oracle.score(nwhip.synth(1, 2 * width), nwhip.synth(2, crows))
-    assert alt["config"]["n1"] == 2 * width
+    alts = res["alt_partitions"]
+    assert res["config"].get("blocks_per_gpu", 1) == blocks
+    if blocks > 1:
+        assert alts["rows_contiguous"]["score"] == want
+    assert alts["cols"]["score"] == oracle.score(nwhip.synth(1, 2 * width), nwhip.synth(2, crows))
+    assert alts["cols"]["config"]["n1"] == 2 * width
 
 
 def test_launch_schedule_never_rewrites_an_unread_buffer():
