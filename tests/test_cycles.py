@@ -37,6 +37,68 @@ def test_cycle_layout():
                                   np.r_[np.arange(4, 8), np.arange(16, 20)].astype(np.int8))
 
 
+# ------------------------------------------------------------------ gloo ranks (CPU)
+def _block_rows(s1, s2_blk, top, row0, scheme):
+    """Rows row0 .. row0 + h of the table given row row0 (`top`): the serial
+    recurrence (serial.cpp:21-33), each row as a running maximum in the w form
+    w = t - GAP * j (numpy restatement for the contract test)."""
+    match, mismatch, gap = scheme
+    h, n1 = s2_blk.size, s1.size
+    t = np.empty((h + 1, n1 + 1), np.int64)
+    t[0] = top
+    j = np.arange(n1 + 1, dtype=np.int64)
+    for i in range(1, h + 1):
+        sub = np.where(s1 == s2_blk[i - 1], match, mismatch)
+        c = np.empty(n1 + 1, np.int64)
+        c[0] = (row0 + i) * gap
+        c[1:] = np.maximum(t[i - 1, :-1] + sub, t[i - 1, 1:] + gap)
+        t[i] = np.maximum.accumulate(c - gap * j) + gap * j
+    return t.astype(np.int32)
+
+
+def _cycle_rank_main(rank, world, port, n1, m, h, scheme, outdir):
+    import datetime
+    import torch.distributed as dist
+    import torch
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
+    s1, s2 = oracle.synth(11, n1), oracle.synth(12, world * m * h)
+    for k in range(m):
+        g = k * world + rank
+        if g == 0:
+            top = np.arange(n1 + 1, dtype=np.int64) * scheme[2]  # serial.cpp:16
+        else:  # the previous block's last row, from rank g-1 mod world (mpi-horz.cpp:28-40 per block)
+            buf = torch.empty(n1 + 1, dtype=torch.int32)
+            dist.recv(buf, src=(rank - 1) % world)
+            top = buf.numpy()
+        blk = _block_rows(s1, s2[g * h:(g + 1) * h], top, g * h, scheme)
+        if g + 1 < world * m:
+            dist.send(torch.from_numpy(blk[-1].copy()), dst=(rank + 1) % world)
+        np.save(os.path.join(outdir, f"block{g}.npy"), blk)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.timeout(240)
+def test_gloo_cycles_reassemble_the_table(tmp_path, world):
+    """The block-cyclic contract over a real gloo world: rank r fills blocks
+    g = k * world + r from the halo row rank g-1 sends (the last rank feeding rank
+    0's next block); the blocks tile the serial table."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    n1, m, h, scheme = 301, 3, 9, (1, -1, -1)
+    mp.spawn(_cycle_rank_main, args=(world, port, n1, m, h, scheme, str(tmp_path)), nprocs=world, join=True)
+    n2 = world * m * h
+    full = oracle.fill(oracle.synth(11, n1), oracle.synth(12, n2), scheme)
+    for g in range(world * m):
+        np.testing.assert_array_equal(np.load(tmp_path / f"block{g}.npy"), full[g * h:(g + 1) * h + 1])
+
+
 @pytest.fixture(scope="module")
 def torch():
     import torch as _t
