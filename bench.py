@@ -8,11 +8,10 @@ table in HBM before the timed region; nothing copied back inside it).
   N = 1 : BASELINE config 3 -- 262144 x 262144 int32 table (275 GB) on one GPU.
   N > 1 : `value` = row bands across ranks (mpi-horz halo contract, BASELINE
           config 4): n1 = 524288 columns and 65536 rows per GPU (weak scaling;
-          N = 8 is 512k x 512k), the rows dealt to the GPUs in --band-blocks
-          blocks each (block-cyclic: every GPU is busy after N blocks instead of
-          N - 1 whole bands); the contiguous bands (mpi-horz's literal layout) and
-          column bands (mpi-vert: 65536 columns per GPU x 524288 rows) run after it
-          as `alt_partitions`.  Launches are enqueued back to back (link-word flow
+          N = 8 is 512k x 512k), contiguous as mpi-horz lays them out; the same
+          rows dealt to the GPUs in 2 blocks each (block-cyclic) and column bands
+          (mpi-vert: 65536 columns per GPU x 524288 rows) run after it as
+          `alt_partitions`.  Launches are enqueued back to back (link-word flow
           control, no host round trip between them);
           fast-needleman-wunsch_amd/nw_bands.py, DESIGN.md "Multi-GPU".
 
@@ -57,9 +56,9 @@ def parse():
     ap.add_argument("--alt-partition", choices=["rows", "cols", "none"], default=None,
                     help="N>1: the alternate legs (`alt_partitions`; default: contiguous row bands "
                          "and column bands)")
-    ap.add_argument("--band-blocks", type=int, default=0,
+    ap.add_argument("--band-blocks", type=int, default=1,
                     help="N>1 row bands: blocks of rows per GPU, dealt round robin (1 = contiguous "
-                         "mpi-horz bands; 0 = auto: blocks of >= 16384 rows, 4 at the defaults)")
+                         "mpi-horz bands; the block-cyclic alternate leg uses 2)")
     ap.add_argument("--kernel", type=int, default=0,
                     help="0 auto, 1 anti-diagonal strips, 2 row-scan panels (nw_params.kernel)")
     ap.add_argument("--col-width", type=int, default=65536,
@@ -295,6 +294,7 @@ def run_sw(args):
     cells = n * n
     table_bytes = 4.0 * (n + 1) * (n + 1)
     fill_ms = sum(fills) / len(fills)
+    traffic, traffic_src = pmc_traffic(f"sw_fill_traceback_{n}x{n}", {1: "strips", 2: "panels"}.get(r.kernel, "?"))
     out = {"metric": "GCUPS (DP cell updates/s) on NxN Smith-Waterman fill + on-device traceback",
            "value": round(cells * args.steps / wall / 1e9, 2), "unit": "GCUPS", "n_gpus": 1,
            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 3),
@@ -307,7 +307,8 @@ def run_sw(args):
            "fill_ms_avg": round(fill_ms, 3), "traceback_ms_avg": round(sum(tbs) / len(tbs), 3),
            "roofline": {"bound": "hbm", "achieved": round(table_bytes / (fill_ms * 1e6), 1), "peak": HBM_PEAK_GBPS,
                         "unit": "GB/s", "frac": round(table_bytes / (fill_ms * 1e6) / HBM_PEAK_GBPS, 4),
-                        "traffic": None, "basis": "fill kernel (+ locate) only"},
+                        "traffic": traffic, "traffic_source": traffic_src,
+                        "basis": "fill kernel (+ best cell / locate) only, 4 B per cell"},
            "kernel": nwhip.version()}
     print(json.dumps(out), flush=True)
 

@@ -442,54 +442,50 @@ def _sweep(args, partition: str, rank: int, world: int, dev: int, scheme, blocks
             "blocks": m, "block_rows": h}
 
 
-# Rows per block below which a block-cyclic launch starves its workers: strips are
-# claimed in (block, strip) order and a block's strips start one hop (64 * NC rows
-# of the anti-diagonal skew) apart, so a block keeps only h / hop of them busy --
-# all 256+ workers need h >= 256 * 64 rows with the (4, 1) strips of a wide block.
-CYCLE_MIN_BLOCK_ROWS = 16384
-
-
-def auto_blocks(args) -> int:
-    """Blocks per rank of the row-band leg: --band-blocks, or (0 = auto) as many as
-    keep every block at least CYCLE_MIN_BLOCK_ROWS rows (1 = contiguous bands);
-    the panel kernel has no block-cyclic launch (1)."""
-    if getattr(args, "kernel", 0) == nwhip.KERNEL_PANELS:
-        return 1
-    m = getattr(args, "band_blocks", 0)
-    if m <= 0:
-        m = max(1, args.band_rows // CYCLE_MIN_BLOCK_ROWS)
-        while m > 1 and args.band_rows % m:
-            m -= 1
-    return m
+# Block-cyclic row bands on one GPU's share of config 4 (524288 x 65536), one launch
+# of m chained blocks against the plain fill (tools/cycle_time.py, profiles/
+# r03p_cycle_time.txt): m = 1 32.3 ms, 2 41.1, 4 58.2, 8 110.1.  Strips are claimed
+# in (block, strip) order and a block's strips start one hop (64 * NC rows of the
+# anti-diagonal skew + the hand-off, ~6.5 us for (4, 1)) apart, so a block of h
+# rows keeps only ~h * pace / hop strips busy: short blocks starve the workers.
+# The multi-GPU model (DESIGN.md section 5) therefore keeps contiguous bands as the
+# main leg and measures 2 blocks per GPU (the only count the model finds no worse)
+# as an alternate.
+CYCLE_ALT_BLOCKS = 2
 
 
 def legs_for(args) -> list:
     """[(name, partition, blocks per rank)] of a multi-GPU bench: the main one
     first (its value is the line's), then the alternates (--alt-partition)."""
     main = getattr(args, "partition", "rows")
-    m = auto_blocks(args)
+    m = max(1, getattr(args, "band_blocks", 1))
+    if getattr(args, "kernel", 0) == nwhip.KERNEL_PANELS:
+        m = 1  # (no block-cyclic launch for the panel kernel)
     rows_main = ("rows_cyclic", "rows", m) if m > 1 else ("rows_contiguous", "rows", 1)
     legs = [rows_main] if main == "rows" else [("cols", "cols", 1)]
     alt = getattr(args, "alt_partition", None)
     if alt == "none":
         return legs
+    cyc_ok = getattr(args, "kernel", 0) != nwhip.KERNEL_PANELS and args.band_rows % CYCLE_ALT_BLOCKS == 0
     if main == "rows":
+        if m == 1 and alt in (None, "rows") and cyc_ok and args.band_rows >= 65536:
+            legs.append(("rows_cyclic", "rows", CYCLE_ALT_BLOCKS))
         if m > 1 and alt in (None, "rows"):
             legs.append(("rows_contiguous", "rows", 1))
         if alt in (None, "cols"):
             legs.append(("cols", "cols", 1))
     elif alt in (None, "rows"):
-        legs.append(rows_main if m > 1 else ("rows_contiguous", "rows", 1))
+        legs.append(rows_main)
     return legs
 
 
 def run_bands(args) -> dict | None:
     """bench.py --gpus N (N > 1) under torch.distributed.run: one rank per GPU.
     `value` = row bands (BASELINE config 4: an n1 x (N * band_rows) table, weak
-    scaling, 512k x 512k at N = 8 with the defaults), by default block-cyclic
-    (--band-blocks blocks of rows per rank, mpi-horz's halo contract per block);
-    the contiguous mpi-horz bands (--band-blocks 1) and the column bands (mpi-vert,
-    N * col_width columns x col_rows rows) run after it as `alt_partitions` unless
+    scaling, 512k x 512k at N = 8 with the defaults), contiguous as mpi-horz lays
+    them out (or block-cyclic with --band-blocks m > 1); block-cyclic rows with
+    CYCLE_ALT_BLOCKS blocks per rank and the column bands (mpi-vert, N * col_width
+    columns x col_rows rows) run after it as `alt_partitions` unless
     --alt-partition none.  Prints and returns the JSON line on rank 0."""
     import torch
     import torch.distributed as dist
@@ -522,8 +518,9 @@ def run_bands(args) -> dict | None:
                                         "roofline")}
     if alts:
         out["alt_partitions"] = alts
-        if name0 == "rows_cyclic" and "rows_contiguous" in alts:  # the same table, two partitions
-            out["rows_legs_agree"] = alts["rows_contiguous"]["score"] == out["score"]
+        rows_legs = [out["score"]] + [alts[k]["score"] for k in ("rows_cyclic", "rows_contiguous") if k in alts]
+        if plan_[0][1] == "rows":  # the same table under both row partitions
+            out["rows_legs_agree"] = len(set(rows_legs)) == 1 if len(rows_legs) > 1 else None
     if cpu_baseline_fn is not None and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_fn(args.cpu_n, scheme)
     print(json.dumps(out), flush=True)

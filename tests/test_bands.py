@@ -192,7 +192,7 @@ def test_two_process_bands_shared_gpu(torch_gpu, kernel, blocks):
     alts = res["alt_partitions"]
     assert res["config"].get("blocks_per_gpu", 1) == blocks
     if blocks > 1:
-        assert alts["rows_contiguous"]["score"] == want
+        assert alts["rows_contiguous"]["score"] == want and res["rows_legs_agree"]
     assert alts["cols"]["score"] == oracle.score(nwhip.synth(1, 2 * width), nwhip.synth(2, crows))
     assert alts["cols"]["config"]["n1"] == 2 * width
 
