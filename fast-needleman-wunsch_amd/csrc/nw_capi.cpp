@@ -766,7 +766,7 @@ int nw_sw_traceback(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *d_s
     // window geometry: band half-width and windows per round (NW_TB_BAND /
     // NW_TB_MAXWIN override them: narrow bands and short rounds for the tests)
     int32_t band = nw::kTbBandDefault, maxwin = nw::kTbMaxWinDefault;
-    if (const char *e = std::getenv("NW_TB_BAND")) band = std::max(1, std::min(128, std::atoi(e)));
+    if (const char *e = std::getenv("NW_TB_BAND")) band = std::max(1, std::min(256, std::atoi(e)));
     if (const char *e = std::getenv("NW_TB_MAXWIN")) maxwin = std::max(1, std::atoi(e));
     maxwin = (int32_t)std::min<int64_t>(maxwin, end_i / 64 + 1);
     if ((st = grow((void **)&c->tbscratch, &c->tbscratch_cap, nw::sw_tb_scratch_bytes(maxwin, band))) != NW_OK)

@@ -97,8 +97,8 @@ size_t sw_tb_scratch_bytes(int32_t maxwin, int32_t band);
 int run_sw_traceback(const int32_t *table, int64_t pitch, int64_t n1, const uint8_t *s1, const uint8_t *s2,
                      int32_t match, int32_t mismatch, int32_t gap, int64_t end_i, int64_t end_j, uint8_t *ops,
                      int64_t ops_cap, void *scratch, int32_t maxwin, int32_t band, int64_t *info, void *stream);
-constexpr int32_t kTbBandDefault = 128;    // band half-width of the traceback windows
-constexpr int32_t kTbMaxWinDefault = 4096; // windows per round (64 rows each)
+constexpr int32_t kTbBandDefault = 256;    // band half-width of the traceback windows (profiles/r03s_tb_geometry.txt)
+constexpr int32_t kTbMaxWinDefault = 512;  // windows per round (64 rows each)
 
 // Launch helpers implemented in nw_fill.hip.  Return hipError_t as int.
 // charmap of s1 into meta, then the row packs (mapped when perm allows it)

@@ -112,13 +112,13 @@ int launch_sw_locate(const int32_t *table, int64_t pitch, int64_t n1, int64_t n2
 // A path that drifts more than B columns off the round's diagonal costs another
 // round (re-centred at the cell where it left); run_sw_traceback loops rounds.
 constexpr int kTbR = 64;                     // rows per window
-constexpr int kTbBMax = 128;                 // band half-width B <= kTbBMax
+constexpr int kTbBMax = 256;                 // band half-width B <= kTbBMax
 constexpr int kTbWMax = 2 * kTbBMax + 1;     // cells per window row, W = 2B + 1
 constexpr int kTbThreads = 512;
 constexpr int kChain = 32;                   // windows per LDS chunk of nw_tb_chain
 enum : uint8_t { kCStop = 0, kCDiag = 1, kCUp = 2, kCLeft = 3, kCBad = 4 };
 enum : uint32_t { kXCont = 0, kXStop = 1, kXOut = 2, kXBad = 3 };
-// exit record: kind 0-1 | moves 2-11 | row 12-18 | column 19-27 (kXCont: the
+// exit record: kind 0-1 | moves 2-11 | row 12-18 | column 19-28 (kXCont: the
 // column entered in the next window; otherwise the cell where the walk ended)
 __device__ __forceinline__ uint32_t xrec(uint32_t kind, uint32_t cnt, uint32_t r, uint32_t x) {
     return kind | (cnt << 2) | (r << 12) | (x << 19);
@@ -173,7 +173,7 @@ __global__ __launch_bounds__(kTbThreads) void nw_tb_windows(const int32_t *__res
         gcd[e] = c;
     }
     __syncthreads();
-    if ((int)threadIdx.x < W) exits[(int64_t)k * W + threadIdx.x] = tb_walk(cd, W, threadIdx.x, [](uint32_t) {});
+    for (int x = threadIdx.x; x < W; x += kTbThreads) exits[(int64_t)k * W + x] = tb_walk(cd, W, x, [](uint32_t) {});
 }
 
 // ctl: [0] ops so far, [1] how the round ended (kXStop / kXCont|kXOut = restart /
