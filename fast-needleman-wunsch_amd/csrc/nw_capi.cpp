@@ -599,6 +599,108 @@ int nw_fill_colband_async(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_
     return launch_fill(c, d_s1, n1, d_s2, n2, p, nullptr, band, d_t, pitch, stream);
 }
 
+// Row band in horizontal strips: the (4, 1) strip kernel on the TRANSPOSED band
+// (the NW table of (s2_band, s1) is the band's transpose, the scores being
+// symmetric), in global row numbers: its "columns" are global rows row0 + 1 ..
+// row0 + R (strips of 256 rows from row0 + 1), its "rows" the band's columns
+// 0..n1; the store waves write the row-major band table (store_strip_tr).
+int nw_fill_tband_async(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *d_s2, int64_t R,
+                        const nw_params *p, const nw_tband *tb, int32_t *d_t, int64_t pitch, void *stream) {
+    if (!c || !d_t || !tb || !d_s1 || !d_s2 || n1 < 1 || R < 1 || n1 >= INT32_MAX || R >= INT32_MAX ||
+        tb->row0 < 0 || tb->row0 + R >= INT32_MAX)
+        return NW_ERR_ARG;
+    if (!valid_params(p)) return NW_ERR_ARG;
+    if (p->mode != NW_MODE_NW || p->kernel == NW_KERNEL_PANELS || (p->substrips != 0 && p->substrips != 4) ||
+        (p->strip_waves != 0 && p->strip_waves != 1))
+        return NW_ERR_UNSUPPORTED;
+    if (tb->tag == 0 || (((uintptr_t)tb->feed_in | (uintptr_t)tb->feed_out) & 7u) != 0) return NW_ERR_ARG;
+    if ((tb->row0 > 0) != (tb->feed_in != nullptr)) return NW_ERR_ARG;
+    if (tb->feed_out && (p->flags & 1)) return NW_ERR_ARG;  // needs the real last row
+    if ((((uintptr_t)d_t + 4u) & 255u) != 0 || pitch % nw::kWave != 0 || pitch < n1 + 4) return NW_ERR_ARG;
+    {  // |w| bound of launch_fill, with the global row
+        const long long m = std::max({std::llabs(p->match), std::llabs(p->mismatch), std::llabs(p->gap)});
+        if ((m + std::llabs(p->gap)) * (long long)(n1 + tb->row0 + R + 2) >= (1LL << 28)) return NW_ERR_ARG;
+    }
+    NW_HIP_TRY(hipSetDevice(c->device));
+    // the transposed band: R + 1 "columns" (global rows row0 .. row0 + R, the first
+    // one the feed), n1 + 1 "rows" (the band's columns)
+    Shape s = make_shape(R, n1, p->waves, 4, 1, c->cus, 1, false, NW_KERNEL_STRIPS);
+    if (!shape_valid(s) || s.nstrips > INT32_MAX / 2 || s.nblocks > INT32_MAX / 2) return NW_ERR_ARG;
+    int st;
+    const size_t gran_need = (size_t)(s.M * s.gstride) * sizeof(uint64_t);
+    bool fresh = false;
+    if ((st = grow((void **)&c->gran, &c->gran_cap, gran_need, &fresh)) != NW_OK) return st;
+    if (fresh) {
+        NW_HIP_TRY(hipMemsetAsync(c->gran, 0, c->gran_cap, (hipStream_t)stream));
+        c->tagbase = 1;
+    }
+    if ((uint64_t)c->tagbase + (uint64_t)s.nstrips + 2u >= 0xFFFFFFF0ull) {
+        NW_HIP_TRY(hipMemsetAsync(c->gran, 0, c->gran_cap, (hipStream_t)stream));
+        c->tagbase = 1;
+    }
+    const int64_t qlen = nw::rowpack_len((int32_t)s.nblocks);
+    if ((st = grow((void **)&c->rowpack, &c->rowpack_cap, (size_t)qlen * 16)) != NW_OK) return st;
+    if ((st = grow((void **)&c->scratch, &c->scratch_cap, (size_t)s.waves * nw::kScratchWords * 4)) != NW_OK)
+        return st;
+    NW_HIP_TRY(hipMemsetAsync(c->ctrl, 0, 32, (hipStream_t)stream));
+    const bool perm_ok = fits_i8(p->match - 2 * p->gap) && fits_i8(p->mismatch - 2 * p->gap) &&
+                         !(p->flags & NW_FLAG_NO_PROFILE);
+    // lanes carry the band's row characters (charmap of s2_band), the row packs the columns' (s1)
+    if (nw::launch_rowpack((const uint8_t *)d_s2, R, (const uint8_t *)d_s1, n1, 0, perm_ok ? 1 : 0, c->meta,
+                           c->rowpack, qlen, stream) != hipSuccess)
+        return NW_ERR_HIP;
+    nw::FillArgs a;
+    std::memset(&a, 0, sizeof a);
+    a.table = d_t;
+    a.pitch = pitch;
+    a.col_end = INT64_MAX;
+    a.strip0 = 0;
+    a.feed_in = tb->feed_in;
+    a.feed_out = tb->feed_out;
+    a.feed_tag = tb->tag;
+    a.rowpack = c->rowpack;
+    a.s1 = (const uint8_t *)d_s2 - tb->row0;  // s1[y - 1] = global row y's character
+    a.n1 = tb->row0 + R;                      // global last row
+    a.n2 = n1;
+    a.row0 = 0;
+    a.col0 = tb->row0 + 1;                    // first swept global row
+    a.nstrips = (int32_t)s.nstrips;
+    a.nblocks = (int32_t)s.nblocks;
+    a.gran = c->gran;
+    a.gstride = s.gstride;
+    a.M = (int32_t)s.M;
+    a.tagbase = c->tagbase;
+    a.ctrl = c->ctrl;
+    a.scratch = c->scratch;
+    a.perm = perm_ok ? 1 : 0;
+    a.charmap = c->meta;
+    a.nprof = (const uint32_t *)(c->meta + 256);
+    a.trace = c->trace;
+    a.match = p->match;
+    a.mismatch = p->mismatch;
+    a.gap = p->gap;
+    a.flags = p->flags;
+    a.timeout_ticks = (uint64_t)(p->timeout_ms > 0 ? p->timeout_ms : 20000) * 100000ull;
+    a.nbl = 1;
+    a.hin0 = 1;
+    a.qstride = qlen * 16;
+    a.hstride = n1 + 1;
+    a.tr = 1;
+    a.tr_y0 = tb->row0;
+    a.tr_pub = (int32_t)(R - 1 - 256 * (s.nstrips - 1));  // the last row's column in the last strip
+    if (nw::launch_fill(a, 4, 1, (int)s.waves, stream) != hipSuccess) return NW_ERR_HIP;
+    if (nw::launch_tband_edges(tb->feed_in, d_t, pitch, n1, R + 1, p->gap, tb->row0, stream) != hipSuccess)
+        return NW_ERR_HIP;
+    c->tagbase += (uint32_t)s.nstrips + 1u;
+    c->last_waves = (int)s.waves;
+    c->last_strips = (int)s.nstrips;
+    c->last_sub = 4;
+    c->last_nc = 1;
+    c->last_col0 = 1;
+    c->last_kernel = NW_KERNEL_STRIPS;
+    return NW_OK;
+}
+
 int64_t nw_feed_bytes(int64_t n2) {
     return n2 < 0 ? 0 : round_up(n2 + 1, nw::kWave) * (int64_t)sizeof(uint64_t);
 }

@@ -102,6 +102,35 @@ int launch_colband_edge(const uint64_t *feed, int32_t *table, int64_t pitch, int
     return (int)hipGetLastError();
 }
 
+// Row band in horizontal strips: the edges the strips do not sweep.  Row 0 is
+// the previous band's last row (the feed the launch consumed, w form in global
+// coordinates: t = w + gap * (x + start)) or, for the first band, the boundary
+// t[0][x] = x * gap (serial.cpp:16); column 0 of rows 1 .. rows-1 is the
+// boundary t[y][0] = (start + y) * gap (serial.cpp:17), start = global row of
+// the band's row 0.
+__global__ __launch_bounds__(256) void nw_tband_edges(const uint64_t *__restrict__ feed,
+                                                      int32_t *__restrict__ table, int64_t pitch, int64_t n1,
+                                                      int64_t rows, int32_t gap, int64_t start) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i <= n1) {
+        int64_t v = (int64_t)gap * i;
+        if (feed != nullptr) {
+            const uint64_t g = __hip_atomic_load(feed + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            v = (int64_t)(int32_t)(uint32_t)g + (int64_t)gap * (i + start);
+        }
+        table[i] = (int32_t)v;
+    }
+    if (i >= 1 && i < rows) table[i * pitch] = (int32_t)((int64_t)gap * (start + i));
+}
+
+int launch_tband_edges(const uint64_t *feed, int32_t *table, int64_t pitch, int64_t n1, int64_t rows,
+                       int32_t gap, int64_t start, void *stream) {
+    const int64_t n = std::max<int64_t>(n1 + 1, rows);
+    hipLaunchKernelGGL(nw_tband_edges, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       feed, table, pitch, n1, rows, gap, start);
+    return (int)hipGetLastError();
+}
+
 // entries of 16 bytes: iteration j <= nblocks + 3 (prefetch of the last one)
 // reads up to index kQOff + 64 * (nblocks + 3) + 48
 int64_t rowpack_len(int32_t nblocks) { return kQOff + 64 * ((int64_t)nblocks + 4) + 16; }

@@ -76,12 +76,28 @@ struct FillArgs {
     int32_t nbl;
     int32_t hin0, hoshift;
     int64_t tstride, qstride, hstride;
+    // Row band in HORIZONTAL strips (nw_fill_tband_async): the launch sweeps the
+    // transposed band -- its strips run along the band's rows, one step per
+    // table column -- so `n1` / `s1` / col0 above describe the band's ROWS in
+    // global row numbers (col0 = first swept global row, s1 biased so that
+    // s1[y - 1] is global row y's character) and `n2` / the row packs its
+    // columns.  Store waves write the real row-major band table (`table`, row 0 =
+    // global row tr_y0).  The feeds carry the band's top row in and its last row
+    // out; tr_pub is the strip-local column of that last row in the last strip.
+    int32_t tr;
+    int32_t tr_pub;
+    int64_t tr_y0;
 };
 bool sw_shape_ok(int substrips, int strip_waves);
 // column band r > 0: local column 0 (global column `start`) from the feed
 // granules, t = w + gap * (i + start), rows 0..n2; asynchronous on `stream`
 int launch_colband_edge(const uint64_t *feed, int32_t *table, int64_t pitch, int64_t n2, int32_t gap,
                         int64_t start, void *stream);
+// horizontal-strip row band: row 0 (x = 0..n1; from the feed granules, w form,
+// or the boundary x*gap when feed is NULL) and column 0 (rows 1..rows-1:
+// (start + y)*gap) of the band table; asynchronous on `stream`
+int launch_tband_edges(const uint64_t *feed, int32_t *table, int64_t pitch, int64_t n1, int64_t rows,
+                       int32_t gap, int64_t start, void *stream);
 // best cell of an SW table: reduce smax[nstrips] and find the first row-major cell
 // holding the maximum (out8[0] = score, out8[1..2] = row, out8[3..4] = column as
 // 64-bit halves); device buffers, asynchronous on `stream`

@@ -240,6 +240,12 @@ struct Lanes {
     uint32_t rc[2];    // read-back address of the right column (see run_iter); grouped
                        // rings: rc[0] = record of lane 63, rc[1] = (lane & 15) - 1
     int32_t rcol;      // right-column value read back, published a few steps later
+    // horizontal-strip band, last strip: the published column is the band's last
+    // row, compute lane a* / column k* (FillArgs::tr_pub) instead of lane 63's
+    // last column: read back from slot (64*HALF + 16c + pofs) mod kR at pbase
+    bool psel;
+    int32_t pofs;
+    uint32_t pbase;
 };
 
 // Where a compute wave's feed comes from.
@@ -429,6 +435,9 @@ __device__ __forceinline__ void run_iter(char *__restrict__ lds, int it, const u
                 } else {
                     // lane i < 16: slot (64*HALF + 16c + i - 1) mod kR, lane 63's last column
                     a = (HALF == 0 && c == 0) ? S.rc[0] : S.rc[1] + (64 * HALF + 16 * c) * L::kSlot;
+                    // (horizontal-strip band: lane a*'s row 64b + 16c + i was written at
+                    // step 64it + 16c + i + a* - 64)
+                    if (S.psel) a = S.pbase + ((uint32_t)(64 * HALF + 16 * c + S.pofs) & (uint32_t)(kR - 1)) * L::kSlot;
                 }
                 S.rcol = *(const int32_t *)(lds + a);
             }
@@ -573,12 +582,13 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
     // its granules (or, for strip 0, the boundary column); later waves take
     // wave j-1's from LDS.  Output: the strip's last wave publishes granules,
     // the others feed wave j+1.
+    // a column band's first strip is fed by the left band (feed_in, feed_tag) --
+    // also strip 0 of a horizontal-strip row band below the first
+    const bool fed = p == A.strip0 && A.feed_in != nullptr;
     Feed F;
-    F.src = j > 0 ? FEED_LDS : p > 0 ? FEED_GRAN : FEED_BOUNDARY;
+    F.src = j > 0 ? FEED_LDS : (p > 0 || fed) ? FEED_GRAN : FEED_BOUNDARY;
     F.ring = (int32_t *)(lds + L::kFeed) + j * kFeedRows;
     F.pub = (const int32_t *)(lds + L::kCtl) + (j > 0 ? j - 1 : 0) * L::kCtlWords + 1;
-    // a column band's first strip is fed by the left band (feed_in, feed_tag)
-    const bool fed = p == A.strip0 && A.feed_in != nullptr;
     const bool feeds = p == A.strip0 + A.nstrips - 1 && A.feed_out != nullptr;
     F.tag = fed ? A.feed_tag : A.tagbase + (uint32_t)B.pq;
     F.gap = gap;
@@ -594,6 +604,19 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
     O.ring = (int32_t *)(lds + L::kFeed) + (j + 1 < NC ? j + 1 : j) * kFeedRows;
     O.pub = ctr + 1;
     O.gap = gap;
+    // horizontal-strip band (FillArgs::tr): the band's last row may sit inside
+    // the last strip -- publish strip-local column tr_pub (one compute wave)
+    S.psel = false;
+    S.pofs = 0;
+    S.pbase = 0;
+    if constexpr (!L::kGrp && NC == 1) {
+        if (A.tr != 0 && feeds) {
+            const int as = A.tr_pub / C, ks = A.tr_pub % C;
+            S.psel = true;
+            S.pofs = (lane & 15) - 64 + as;
+            S.pbase = (uint32_t)(as * 4 * C + 4 * ks);
+        }
+    }
     const int32_t *next_done = ctr + L::kCtlWords + 2;  // iterations done by wave j+1
 
     const uint64_t *gin = (fed ? A.feed_in : A.gran + (int64_t)((B.pq + A.M - 1) % A.M) * A.gstride) + lane;
@@ -904,6 +927,92 @@ __device__ __forceinline__ void store_strip(const FillArgs &A, char *__restrict_
     }
 }
 
+// Store wave q of a HORIZONTAL strip (row band in horizontal strips,
+// nw_fill_tband_async; the (4, 1) shape).  The strip runs along the band's
+// rows: ring row x (step s holds rows x = s - a of compute lanes a) is table
+// COLUMN x, and compute lane a's 16-byte piece holds table rows y = c0 + 4a + k,
+// k < 4 (global numbering; local row y - tr_y0).  Columns leave in batches of 32
+// (x = 1 + 32b .. +31: 128-byte row segments, aligned when column 1 starts a
+// 256-byte line), dealt round robin to the kSPR store waves.  Store lane
+// (g, l8) = (lane / 8, lane % 8) takes, for each block of 8 compute lanes
+// a = 8 blk + l8, the 4 x 4 tile rows 4a .. 4a+3 x columns x0 + 4g .. +3 with
+// four ds_read_b128 (slot (x + a) mod kR, byte 16a: the 8 lanes the LDS serves
+// together hit 8 distinct 16-byte bank groups) and stores it as four 16-byte row
+// pieces: one store instruction = 8 rows x 128 bytes.  A wave publishes its
+// first batch start before reading anything (rows below it are none of its
+// business): with 3 waves x 32 columns the ring's slack would otherwise run out
+// before the third wave's first batch is complete.
+template <int C, int NC>
+__device__ __forceinline__ void store_strip_tr(const FillArgs &A, char *__restrict__ lds, const Blk &B,
+                                               int q, int lane) {
+    static_assert(C == 4 && NC == 1, "horizontal strips: the (4, 1) shape");
+    typedef Lay<C, NC> L;
+    constexpr int BATCH = 32, NS = L::kSPR, NBLK = 8;
+    static_assert(BATCH + 63 + L::kChk + L::kPub <= kR, "a batch must fit the ring's slack");
+    const int p = B.pk;
+    int32_t *ctr = (int32_t *)(lds + L::kCtl);
+    const int64_t c0 = A.col0 + (int64_t)p * (64 * C);  // global row of compute lane 0's first piece
+    const int32_t nx = (int32_t)(A.n2 + 1);             // ring rows = table columns 0 .. n2
+    const bool timing = (A.flags & 1) != 0;
+    const int g = lane >> 3, l8 = lane & 7;
+    const uint32_t ug = (uint32_t)A.gap;
+    int32_t *mine = ctr + 3 + q;
+    const int32_t f0 = 1 + q * BATCH;
+    ctr_store(mine, f0);
+    if (A.flags & 8) {  // debug: no store waves (compute-pace probe, timing only)
+        ctr_store(mine, kDone);
+        return;
+    }
+    // rows of this lane: y = c0 + 4 (8 blk + l8) + k; valid while y <= n1 (the band's last row)
+    uint32_t rmask = 0;
+#pragma unroll
+    for (int blk = 0; blk < NBLK; ++blk)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            rmask |= (c0 + 4 * (8 * blk + l8) + k <= A.n1 ? 1u : 0u) << (4 * blk + k);
+    const int64_t rowb = timing ? 0 : A.pitch;  // int32 elements per table row
+    int32_t *base = timing ? A.scratch + (int64_t)blockIdx.x * kScratchWords + 4 * g
+                           : B.table + (c0 - A.tr_y0 + 4 * l8) * A.pitch + 4 * g;
+    // GAP * (x + y) of element (blk, e, k) = kb + ug * (32 blk + e + k) + ug * f
+    const uint32_t kb = ug * (uint32_t)(4 * g) + ug * (uint32_t)(c0 + 4 * l8);
+    const uint32_t bpos = (uint32_t)l8 * 16u;  // byte of compute lane a = 8 blk + l8 within its slot: + 128 blk
+    int32_t avail = 0;
+    for (int32_t f = f0; f < nx; f += NS * BATCH) {
+        const int32_t want = min(f + BATCH, nx);
+        if (avail < want) {
+            int32_t sa = __builtin_amdgcn_readfirstlane(ctr_load(ctr));
+            if (sa != kDone && sa - 63 < want) sa = wait_counter(ctr, want + 63, A.ctrl, 8, A.timeout_ticks);
+            avail = (sa == kDone || sa == kDead) ? nx : min(sa - 63, nx);
+            lds_order();  // ring reads after the counter that released them
+        }
+        u32x4 v[NBLK][4];
+#pragma unroll
+        for (int blk = 0; blk < NBLK; ++blk)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const uint32_t slot = (uint32_t)(f + 4 * g + e + 8 * blk + l8) & (uint32_t)(kR - 1);
+                v[blk][e] = *(const u32x4 *)(lds + slot * L::kSlot + bpos + 128u * blk);
+            }
+        // the batch is in registers: release its ring rows before the stores
+        lds_order();
+        ctr_store(mine, f + NS * BATCH);
+        const bool xok = f + 4 * g <= A.n2;  // (a piece reaching past column n2 stays in the pitch slack)
+        const uint32_t kf = kb + ug * (uint32_t)f;
+        int32_t *col = timing ? base : base + f;
+#pragma unroll
+        for (int blk = 0; blk < NBLK; ++blk)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                u32x4 o;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o[e] = v[blk][e][k] + kf + ug * (uint32_t)(32 * blk + e + k);
+                if (xok && ((rmask >> (4 * blk + k)) & 1u))
+                    *(u32x4 *)(col + (int64_t)(32 * blk + k) * rowb) = o;
+            }
+    }
+    ctr_store(mine, kDone);
+}
+
 // Store wave q of compute wave j on strip p, GROUPED ring (C == 1: 64 columns,
 // records of 4 steps, lane slots gpos -- see grp_pos).  One store instruction
 // covers 8 rows x 32 columns: lane (r, q8) = (lane / 8, lane % 8) takes row
@@ -1181,10 +1290,16 @@ __global__ __launch_bounds__((64 * Lay<C, NC>::kWaves)) void nw_fill_strips(Fill
             }
         } else {
             const int b = wave - NC;
-            if constexpr (L::kGrp)
+            if constexpr (L::kGrp) {
                 store_strip_grp<NC>(A, lds, B, b % NC, b / NC, lane);
-            else
+            } else if constexpr (C == 4 && NC == 1) {
+                if (A.tr != 0)
+                    store_strip_tr<C, NC>(A, lds, B, b, lane);  // (row band in horizontal strips)
+                else
+                    store_strip<C, NC>(A, lds, B, 0, b, lane);
+            } else {
                 store_strip<C, NC>(A, lds, B, b % NC, b / NC, lane);
+            }
         }
         __syncthreads();  // the rings and counters are reused by the next strip
     }

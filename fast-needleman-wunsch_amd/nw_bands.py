@@ -123,6 +123,55 @@ class LocalBands:
             c.close()
 
 
+class LocalTBands:
+    """P row bands of one (n2+1) x (n1+1) table on one device in HORIZONTAL strips
+    (nw_fill_tband_async): the mpi-horz partition and row-major band tables of
+    LocalBands, each band swept as 256-row strips along the columns, band r-1's
+    last row fed to band r column by column through a Feed(n1) buffer.  Each band
+    gets 1/P of the resident (4, 1) workers so that all bands are co-resident."""
+
+    def __init__(self, n1: int, n2: int, nbands: int, device: int = 0):
+        import torch
+        self.n1, self.n2, self.P, self.device = n1, n2, nbands, device
+        self.layout = plan(n2, nbands)
+        if any(rows < 2 for rows, _ in self.layout):
+            raise ValueError(f"{nbands} horizontal-strip bands need at least one row below each halo")
+        self.tables = [nwhip.Context.alloc_table(n1, rows - 1) for rows, _ in self.layout]
+        self.feeds = [None] + [nwhip.Feed(n1, device) for _ in range(nbands - 1)]
+        self.ctxs = [nwhip.Context(device) for _ in range(nbands)]
+        self.streams = [torch.cuda.Stream(device) for _ in range(nbands)]
+        self.waves = max(1, resident_waves(device, 4, 1) // nbands)
+        self.tag = 0
+
+    def fill(self, d_s1, d_s2, scheme=(1, 0, -1), flags: int = 0, timeout_ms: int = 0) -> int:
+        """Fill every band; returns the final score t[n2][n1] (last band's last cell)."""
+        import torch
+        assert int(d_s1.numel()) == self.n1 and int(d_s2.numel()) == self.n2
+        self.tag += 1
+        cur = torch.cuda.current_stream(self.device)
+        for r, ((rows, start), st) in enumerate(zip(self.layout, self.streams)):
+            st.wait_stream(cur)
+            self.ctxs[r].fill_tband(
+                d_s1, d_s2[start:start + rows - 1], self.tables[r], row0=start,
+                feed_in=self.feeds[r].ptr if r > 0 else None,
+                feed_out=self.feeds[r + 1].ptr if r + 1 < self.P else None,
+                tag=self.tag, scheme=scheme, waves=self.waves, stream=st, flags=flags, timeout_ms=timeout_ms)
+        for r, st in enumerate(self.streams):
+            s = self.ctxs[r].status(st)
+            if s != nwhip.NW_OK:
+                raise nwhip.NwError(s, f"horizontal-strip band {r}")
+            cur.wait_stream(st)
+        rows, _ = self.layout[-1]
+        return int(self.tables[-1][rows - 1, self.n1].item())
+
+    def close(self):
+        for f in self.feeds:
+            if f is not None:
+                f.free()
+        for c in self.ctxs:
+            c.close()
+
+
 def cycle_layout(n2: int, nranks: int, nblk: int):
     """Block-cyclic row bands (nw_fill_band_cycle_async): the n2 rows below row 0
     cut into nranks * nblk blocks of h rows, global block g = k * nranks + r being
@@ -330,8 +379,9 @@ def _sweep(args, partition: str, rank: int, world: int, dev: int, scheme, blocks
     import torch.distributed as dist
 
     cols = partition == "cols"
-    kernel = getattr(args, "kernel", 0)
-    m = max(1, blocks) if not cols else 1
+    hrows = partition == "hrows"  # row bands in horizontal strips (nw_fill_tband_async)
+    kernel = getattr(args, "kernel", 0) if not hrows else nwhip.KERNEL_STRIPS
+    m = max(1, blocks) if partition == "rows" else 1
     cyc = m > 1
     ctx = nwhip.Context(dev)
     stream = torch.cuda.current_stream()
@@ -356,6 +406,18 @@ def _sweep(args, partition: str, rank: int, world: int, dev: int, scheme, blocks
         links_in = [nwhip.Halo(n1, dev, regions=m) for _ in range(2)]
         sub, nc = band_shape(n1, h, args.substrips, args.strip_waves)
         rows, start, ncols = h + 1, ((m - 1) * world + rank) * h, n1 + 1
+    elif hrows:
+        # row bands (mpi-horz, BASELINE config 4) swept in horizontal strips: the
+        # halo is a feed of one granule per column
+        n1 = args.band_cols
+        n2 = world * args.band_rows
+        rows, start = nwhip.band_layout(n2, world, rank)
+        s1 = torch.from_numpy(nwhip.synth(1, n1)).cuda()
+        s2 = torch.from_numpy(nwhip.synth(2, n2)[start:start + rows - 1].copy()).cuda()
+        table = nwhip.Context.alloc_table(n1, rows - 1)
+        links_in = [nwhip.Feed(n1, dev) for _ in range(2)] if rank > 0 else None
+        sub, nc = 4, 1
+        ncols = n1 + 1
     else:
         # row bands (mpi-horz, BASELINE config 4): rank r owns band_rows rows
         n1 = args.band_cols
@@ -396,6 +458,10 @@ def _sweep(args, partition: str, rank: int, world: int, dev: int, scheme, blocks
         if cols:
             ctx.fill_colband(s1, s2, table, world, rank, feed_in=links_in[b].ptr if links_in else None,
                              feed_out=out_bufs[b] if out_bufs else None, **kw)
+        elif hrows:
+            ctx.fill_tband(s1, s2, table, row0=start, feed_in=links_in[b].ptr if links_in else None,
+                           feed_out=out_bufs[b] if out_bufs else None, tag=k, scheme=scheme, waves=waves,
+                           stream=stream)
         elif cyc:
             ctx.fill_band_cycle(s1, s2, h, table, halo_in=links_in[b].ptr, halo_out=out_bufs[b],
                                 hin_first=rank > 0, hout_shift=int(rank == world - 1), row0_max=start, **kw)
@@ -456,22 +522,33 @@ CYCLE_ALT_BLOCKS = 2
 
 def legs_for(args) -> list:
     """[(name, partition, blocks per rank)] of a multi-GPU bench: the main one
-    first (its value is the line's), then the alternates (--alt-partition)."""
+    first (its value is the line's), then the alternates (--alt-partition).
+    Row bands (BASELINE config 4, mpi-horz's contiguous partition) are swept in
+    horizontal strips by default (--band-sweep): band r+1 then starts a strip hop
+    after band r instead of band r's whole height; the
+    vertical sweep of the same bands, the block-cyclic rows and the column bands
+    run as alternates."""
     main = getattr(args, "partition", "rows")
+    kernel = getattr(args, "kernel", 0)
     m = max(1, getattr(args, "band_blocks", 1))
-    if getattr(args, "kernel", 0) == nwhip.KERNEL_PANELS:
+    if kernel == nwhip.KERNEL_PANELS:
         m = 1  # (no block-cyclic launch for the panel kernel)
-    rows_main = ("rows_cyclic", "rows", m) if m > 1 else ("rows_contiguous", "rows", 1)
+    horiz_ok = kernel != nwhip.KERNEL_PANELS  # (horizontal strips: the (4, 1) strip kernel)
+    horiz = horiz_ok and getattr(args, "band_sweep", "horizontal") == "horizontal"
+    rows_h = ("rows_horizontal", "hrows", 1)
+    rows_v = ("rows_contiguous", "rows", 1)
+    rows_main = ("rows_cyclic", "rows", m) if m > 1 else rows_h if horiz else rows_v
     legs = [rows_main] if main == "rows" else [("cols", "cols", 1)]
     alt = getattr(args, "alt_partition", None)
     if alt == "none":
         return legs
-    cyc_ok = getattr(args, "kernel", 0) != nwhip.KERNEL_PANELS and args.band_rows % CYCLE_ALT_BLOCKS == 0
+    cyc_ok = kernel != nwhip.KERNEL_PANELS and args.band_rows % CYCLE_ALT_BLOCKS == 0
     if main == "rows":
-        if m == 1 and alt in (None, "rows") and cyc_ok and args.band_rows >= 65536:
-            legs.append(("rows_cyclic", "rows", CYCLE_ALT_BLOCKS))
-        if m > 1 and alt in (None, "rows"):
-            legs.append(("rows_contiguous", "rows", 1))
+        if alt in (None, "rows"):
+            cands = ([rows_h] if horiz_ok else []) + [rows_v]
+            if cyc_ok and args.band_rows >= 65536:
+                cands.append(("rows_cyclic", "rows", CYCLE_ALT_BLOCKS))
+            legs += [c for c in cands if c[0] != rows_main[0]]
         if alt in (None, "cols"):
             legs.append(("cols", "cols", 1))
     elif alt in (None, "rows"):
@@ -518,8 +595,9 @@ def run_bands(args) -> dict | None:
                                         "roofline")}
     if alts:
         out["alt_partitions"] = alts
-        rows_legs = [out["score"]] + [alts[k]["score"] for k in ("rows_cyclic", "rows_contiguous") if k in alts]
-        if plan_[0][1] == "rows":  # the same table under both row partitions
+        rows_legs = [out["score"]] + [alts[k]["score"] for k in ("rows_horizontal", "rows_cyclic", "rows_contiguous")
+                                      if k in alts]
+        if plan_[0][1] in ("rows", "hrows"):  # the same table under every row partition
             out["rows_legs_agree"] = len(set(rows_legs)) == 1 if len(rows_legs) > 1 else None
     if cpu_baseline_fn is not None and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_fn(args.cpu_n, scheme)
@@ -557,6 +635,13 @@ def _line(args, world: int, scheme, part: str, ms: list) -> dict:
         cfg = {"workload": f"nw_fill_colbands_{n2}x{n1}", "col_width": args.col_width,
                "parallelism": f"column bands x{world} (mpi-vert)",
                "halo": "in-kernel xGMI peer stores of the band's right column, 16 rows at a time", **common}
+    elif part == "hrows":
+        cfg = {"workload": f"nw_fill_rowbands_{n2}x{n1}", "band_rows": args.band_rows,
+               "parallelism": f"row bands x{world}, contiguous (mpi-horz, BASELINE config 4), each band swept in "
+                              "horizontal strips of 256 rows (nw_fill_tband_async)",
+               "halo": "in-kernel xGMI peer stores of the band's last row, 16 columns at a time, as the band's "
+                       "last strip produces it",
+               **common}
     elif m0["blocks"] > 1:
         cfg = {"workload": f"nw_fill_rowbands_{n2}x{n1}", "band_rows": args.band_rows,
                "blocks_per_gpu": m0["blocks"], "block_rows": m0["block_rows"],

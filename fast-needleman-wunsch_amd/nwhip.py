@@ -36,7 +36,7 @@ EXPORTS = ["nw_params_default", "nw_strerror", "nw_version", "nw_fill", "nw_tabl
            "nw_debug_trace_words", "nw_colband_layout", "nw_feed_bytes", "nw_feed_alloc",
            "nw_fill_colband_async", "nw_link_alloc", "nw_link_wait_async", "nw_link_signal_async",
            "nw_link_status", "nw_host_warmup", "nw_host_release", "nw_halo_alloc_regions",
-           "nw_fill_band_cycle_async"]
+           "nw_fill_band_cycle_async", "nw_fill_tband_async"]
 IPC_HANDLE_BYTES = 64
 
 
@@ -81,6 +81,12 @@ class NwColBand(ctypes.Structure):
     """nw_colband (include/nw_hip.h): feed granule buffers of one column band."""
     _fields_ = [("feed_in", ctypes.c_void_p), ("feed_out", ctypes.c_void_p), ("tag", ctypes.c_uint32),
                 ("nbands", ctypes.c_int32), ("r", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class NwTBand(ctypes.Structure):
+    """nw_tband (include/nw_hip.h): feed granule buffers of one row band in horizontal strips."""
+    _fields_ = [("feed_in", ctypes.c_void_p), ("feed_out", ctypes.c_void_p), ("tag", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32), ("row0", ctypes.c_int64)]
 
 
 class NwError(RuntimeError):
@@ -184,6 +190,9 @@ def lib() -> ctypes.CDLL:
     L.nw_fill_colband_async.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
                                         ctypes.c_int64, ctypes.POINTER(NwParams), ctypes.POINTER(NwColBand),
                                         ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+    L.nw_fill_tband_async.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                      ctypes.c_int64, ctypes.POINTER(NwParams), ctypes.POINTER(NwTBand),
+                                      ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
     L.nw_link_alloc.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
     L.nw_link_wait_async.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int32, ctypes.c_void_p]
     L.nw_link_signal_async.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
@@ -645,6 +654,29 @@ class Context:
                                          ctypes.c_void_p(stream.cuda_stream))
         if st != NW_OK:
             raise NwError(st, "nw_fill_colband_async")
+
+    def fill_tband(self, d_s1, d_s2_band, table, row0: int = 0, feed_in=None, feed_out=None, tag: int = 1,
+                   scheme=(1, 0, -1), waves: int = 0, stream=None, flags: int = 0,
+                   timeout_ms: int = 0) -> None:
+        """Launch one row band in horizontal strips (asynchronous, nw_fill_tband_async):
+        the nw_fill_band contract (table: alloc_table(n1, len(d_s2_band)), row 0 =
+        global row `row0` = the previous band's last row) with the band's rows swept
+        as 256-row strips along the columns.  feed_in / feed_out: Feed(n1) buffers'
+        addresses (raw ints, e.g. peer memory from ipc_open_handle) or None at the ends."""
+        import torch
+        n1, n2 = int(d_s1.numel()), int(d_s2_band.numel())
+        assert table.dtype == torch.int32 and table.is_contiguous()
+        assert table.shape[0] >= table_rows(n2) and table.shape[1] >= n1 + 1 and table.shape[1] % 64 == 0
+        if stream is None:
+            stream = torch.cuda.current_stream(table.device)
+        b = NwTBand(feed_in, feed_out, int(tag), 0, int(row0))
+        p = params(scheme, waves, self.device, flags, 0, 0, timeout_ms)
+        st = lib().nw_fill_tband_async(self._h, ctypes.c_void_p(d_s1.data_ptr() if n1 else 0), n1,
+                                       ctypes.c_void_p(d_s2_band.data_ptr() if n2 else 0), n2, ctypes.byref(p),
+                                       ctypes.byref(b), ctypes.c_void_p(table.data_ptr()), table.shape[1],
+                                       ctypes.c_void_p(stream.cuda_stream))
+        if st != NW_OK:
+            raise NwError(st, "nw_fill_tband_async")
 
     def sw_traceback(self, d_s1, d_s2, table, end, scheme=(1, -1, -1)):
         """Traceback of a device SW table (filled with mode=MODE_SW) from end = (i, j):

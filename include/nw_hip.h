@@ -369,6 +369,37 @@ int nw_fill_colband_async(nw_ctx *ctx, const int8_t *d_s1, int64_t n1, const int
                           int64_t n2, const nw_params *p, const nw_colband *band, int32_t *d_t,
                           int64_t pitch, void *stream);
 
+/* Row bands in HORIZONTAL strips (the config-4 row-band case, short chain) ----
+ * The same contract and partition as nw_fill_band_async (src/mpi/mpi-horz.cpp:4-99,
+ * nw_band_layout: band r's row 0 is band r-1's last row) and the same row-major
+ * band table, but the band is swept the other way round: its rows are cut into
+ * strips of 256 rows that run left to right along the columns, one step per
+ * column (the (4, 1) strip kernel on the transposed band, whose store waves
+ * write the row-major table in 128-byte row pieces).  Band r's first strip takes
+ * row 0 from `feed_in` column by column as band r-1's last strip produces it
+ * (granules {tag:32 | w:32}, one per column 0..n1: nw_feed_alloc(device, n1)), and
+ * band r's last strip publishes its last row into `feed_out`.  Band r+1 therefore
+ * starts 256 rows (a strip's 64-column hop) after band r instead of after band
+ * r's whole height -- the reference streams its halo in 1280-column chunks for
+ * the same reason (mpi-horz.cpp:28-40).  After the fill, row 0 is written from
+ * feed_in (the boundary j*gap for band 0) and column 0 is the boundary i*gap.
+ * d_t: (n2_band + 1) rows laid out like nw_table_offset's (column 1 starts a
+ * 256-byte line), pitch >= nw_table_pitch(n1); d_s2_band: the band's n2_band side
+ * characters (global rows row0 + 1 ..).  NW mode, strips (4, 1) only
+ * (NW_ERR_UNSUPPORTED otherwise).  Asynchronous on `stream`. */
+typedef struct nw_tband {
+    const uint64_t *feed_in;  /* NULL: first band (row 0 = the boundary j*gap)     */
+    uint64_t *feed_out;       /* NULL: last band                                    */
+    uint32_t tag;             /* launch tag, as nw_colband.tag                      */
+    uint32_t reserved;
+    int64_t row0;             /* global row of the band's row 0 (nw_band_layout start;
+                                 0 exactly when feed_in is NULL)                    */
+} nw_tband;
+
+int nw_fill_tband_async(nw_ctx *ctx, const int8_t *d_s1, int64_t n1, const int8_t *d_s2_band,
+                        int64_t n2_band, const nw_params *p, const nw_tband *band, int32_t *d_t,
+                        int64_t pitch, void *stream);
+
 /* Cross-process device pointers (one process per GPU): export a device
  * allocation, open a peer's export.  Handles are NW_IPC_HANDLE_BYTES bytes. */
 #define NW_IPC_HANDLE_BYTES 64

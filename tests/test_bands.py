@@ -165,8 +165,9 @@ def test_local_bands_32k_score(torch_gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kernel,blocks", [(1, 1), (2, 1), (1, 4)])
-def test_two_process_bands_shared_gpu(torch_gpu, kernel, blocks):
+@pytest.mark.parametrize("kernel,blocks,sweep", [(1, 1, "horizontal"), (1, 1, "vertical"), (2, 1, "vertical"),
+                                                 (1, 4, "horizontal")])
+def test_two_process_bands_shared_gpu(torch_gpu, kernel, blocks, sweep):
     """The bench's multi-process path end to end on one GPU: 2 ranks (torch.distributed.run,
     gloo control plane), IPC-mapped halo / feed buffers alternating by launch parity,
     link-word flow control between back-to-back launches, in-kernel halo stores; the
@@ -181,7 +182,7 @@ def test_two_process_bands_shared_gpu(torch_gpu, kernel, blocks):
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "2",
            "--share-gpu", "--partition", "rows", "--band-rows", str(rows), "--band-blocks", str(blocks),
            "--band-cols", str(n1), "--col-width", str(width), "--col-rows", str(crows),
-           "--kernel", str(kernel), "--no-cpu-baseline"]
+           "--kernel", str(kernel), "--band-sweep", sweep, "--no-cpu-baseline"]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-3000:]
     line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1]
@@ -191,10 +192,32 @@ def test_two_process_bands_shared_gpu(torch_gpu, kernel, blocks):
     assert res["score"] == want and res["n_gpus"] == 2 and res["config"]["n2"] == n2
     alts = res["alt_partitions"]
     assert res["config"].get("blocks_per_gpu", 1) == blocks
-    if blocks > 1:
+    if blocks > 1 or (sweep == "horizontal" and kernel == 1):
         assert alts["rows_contiguous"]["score"] == want and res["rows_legs_agree"]
+    if kernel == 1:  # the horizontal sweep of the same bands: main leg or alternate
+        hz = res if (sweep == "horizontal" and blocks == 1) else alts["rows_horizontal"]
+        assert hz["score"] == want and "horizontal strips" in hz["config"]["parallelism"]
     assert alts["cols"]["score"] == oracle.score(nwhip.synth(1, 2 * width), nwhip.synth(2, crows))
     assert alts["cols"]["config"]["n1"] == 2 * width
+
+
+@pytest.mark.parametrize("kw,want", [
+    ({}, ["rows_horizontal", "rows_contiguous", "rows_cyclic", "cols"]),
+    ({"band_sweep": "vertical"}, ["rows_contiguous", "rows_horizontal", "rows_cyclic", "cols"]),
+    ({"band_blocks": 4}, ["rows_cyclic", "rows_horizontal", "rows_contiguous", "cols"]),
+    ({"kernel": 2}, ["rows_contiguous", "cols"]),
+    ({"partition": "cols"}, ["cols", "rows_horizontal"]),
+    ({"alt_partition": "none"}, ["rows_horizontal"]),
+    ({"band_rows": 704}, ["rows_horizontal", "rows_contiguous", "cols"]),
+])
+def test_bench_legs(kw, want):
+    """bench.py --gpus N: the row-band leg that is `value` (config 4: contiguous mpi-horz bands,
+    horizontal strips unless --band-sweep vertical or --band-blocks m > 1) and the alternates."""
+    import argparse
+    a = dict(partition="rows", kernel=0, band_blocks=1, band_sweep="horizontal", alt_partition=None,
+             band_rows=65536)
+    a.update(kw)
+    assert [name for name, _, _ in nw_bands.legs_for(argparse.Namespace(**a))] == want
 
 
 def test_launch_schedule_never_rewrites_an_unread_buffer():

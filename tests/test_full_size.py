@@ -193,16 +193,18 @@ def test_128k_every_row_by_strip_shape(torch, ctx, strip):
 
 @pytest.mark.gpu
 @pytest.mark.slow
-def test_config4_band_geometry(torch):
+@pytest.mark.parametrize("sweep", ["vertical", "horizontal"])
+def test_config4_band_geometry(torch, sweep):
     """BASELINE config 4's row bands (524288 columns, 8 bands, mpi-horz partition) with
     4096 rows per band, concurrently on one device through the in-kernel halo hand-off
-    (the 8-GPU run uses the same kernels with the halo in peer HBM): every row of every
-    band against the whole-table golden rows."""
+    (the 8-GPU run uses the same kernels with the halo in peer HBM), swept in vertical
+    strips (LocalBands) and in horizontal strips (LocalTBands, the bench's main leg):
+    every row of every band against the whole-table golden rows."""
     import nw_bands
     n1, n2, P = 524288, 32767, 8
     g = big_rows(n1, n2, (1, 0, -1))
     torch.cuda.empty_cache()
-    lb = nw_bands.LocalBands(n1, n2, P)
+    lb = nw_bands.LocalBands(n1, n2, P) if sweep == "vertical" else nw_bands.LocalTBands(n1, n2, P)
     try:
         score = lb.fill(torch.from_numpy(nwhip.synth(1, n1)).cuda(),
                         torch.from_numpy(nwhip.synth(2, n2)).cuda())

@@ -1,0 +1,153 @@
+"""Row bands in horizontal strips (nw_fill_tband_async): the mpi-horz contract
+(src/mpi/mpi-horz.cpp:4-99, mpi-horz-driver.cpp:31-32,88-90) with each band swept
+as 256-row strips along the columns, band r-1's last row fed to band r column by
+column.
+
+GPU (-m gpu): LocalTBands -- several bands concurrently on one device through
+the in-kernel feed hand-off -- bit-exact against the oracle's whole table (the
+serial.cpp:4-36 restatement) on ragged shapes, every scheme form, repeated
+launches, a 32k config-2 score and every row of a config-4-width band set; the
+argument refusals.  The multi-process leg is covered by test_bands.py's
+shared-GPU bench test.
+"""
+import ctypes
+import sys
+
+import numpy as np
+import pytest
+
+import nwhip
+import oracle
+from conftest import PKG
+
+sys.path.insert(0, PKG)
+import nw_bands  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def torch_gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def _check(torch, n1, n2, P, scheme, seed, alphabet=4):
+    rng = np.random.default_rng(seed)
+    s1 = rng.integers(1, alphabet + 1, n1).astype(np.int8)
+    s2 = rng.integers(1, alphabet + 1, n2).astype(np.int8)
+    tb = nw_bands.LocalTBands(n1, n2, P)
+    try:
+        score = tb.fill(torch.from_numpy(s1).cuda(), torch.from_numpy(s2).cuda(), scheme)
+        full = oracle.fill(s1, s2, scheme)
+        for r, (rows, start) in enumerate(tb.layout):
+            got = tb.tables[r][:rows, :n1 + 1].cpu().numpy()
+            np.testing.assert_array_equal(got, full[start:start + rows], err_msg=f"band {r}")
+        assert score == full[-1, -1]
+    finally:
+        tb.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n1,n2,P", [(300, 200, 1), (300, 200, 2), (1000, 777, 3), (640, 130, 4),
+                                     (129, 40, 1), (64 * 37 + 5, 999, 5), (5, 600, 3), (4100, 1300, 2),
+                                     (33, 257, 1), (1, 513, 2), (2000, 20, 8), (97, 1025, 4)])
+@pytest.mark.parametrize("scheme", [(1, 0, -1), (1, -1, -1), (2, -1, -2)])
+def test_local_tbands_vs_oracle(torch_gpu, n1, n2, P, scheme):
+    """Partial first/last strips, bands of a few rows, 1-column tables, widths that are
+    not a multiple of the 32-column store batch; the v_perm form (scores - 2 GAP
+    in int8) and the compare forms (UNIT: match - mismatch == 1, GEN: (2,-1,-2))."""
+    _check(torch_gpu, n1, n2, P, scheme, n1 * 31 + n2 + P)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scheme", [(1, 0, -1), (3, -2, -1), (1, -1, 0), (2, 1, 1)])
+def test_local_tbands_alphabets_and_schemes(torch_gpu, scheme):
+    """More than kMaxPerm distinct row characters (the compare fallback), gap 0 and a
+    positive gap."""
+    _check(torch_gpu, 700, 900, 3, scheme, 5, alphabet=20)
+
+
+@pytest.mark.gpu
+def test_local_tbands_repeated_launches(torch_gpu):
+    """Tags advance per launch; stale feed granules of earlier launches are never taken."""
+    torch = torch_gpu
+    n1, n2, P = 2000, 1500, 3
+    tb = nw_bands.LocalTBands(n1, n2, P)
+    try:
+        for seed in range(4):
+            rng = np.random.default_rng(seed)
+            s1 = rng.integers(1, 5, n1).astype(np.int8)
+            s2 = rng.integers(1, 5, n2).astype(np.int8)
+            score = tb.fill(torch.from_numpy(s1).cuda(), torch.from_numpy(s2).cuda())
+            full = oracle.fill(s1, s2)
+            assert score == full[-1, -1]
+            for r, (rows, start) in enumerate(tb.layout):
+                np.testing.assert_array_equal(tb.tables[r][:rows, :n1 + 1].cpu().numpy(),
+                                              full[start:start + rows])
+    finally:
+        tb.close()
+
+
+@pytest.mark.gpu
+def test_local_tbands_32k_score(torch_gpu):
+    """BASELINE config-2 inputs split into 4 concurrent horizontal-strip bands."""
+    torch = torch_gpu
+    n = 32768
+    s1, s2 = nwhip.synth(1, n), nwhip.synth(2, n)
+    tb = nw_bands.LocalTBands(n, n, 4)
+    try:
+        score = tb.fill(torch.from_numpy(s1).cuda(), torch.from_numpy(s2).cuda())
+        assert score == 13394  # reference serial.cpp on the same inputs (synth_scores.json)
+        sc, lr, lc, rs, rw = oracle.score(s1, s2, want_rows=True)
+        for r, (rows, start) in enumerate(tb.layout):
+            sums, wsums = oracle.row_checksums(tb.tables[r][:rows, :n + 1].cpu().numpy())
+            np.testing.assert_array_equal(sums, rs[start:start + rows], err_msg=f"band {r} sums")
+            np.testing.assert_array_equal(wsums, rw[start:start + rows], err_msg=f"band {r} wsums")
+        rows, _ = tb.layout[-1]
+        np.testing.assert_array_equal(tb.tables[-1][rows - 1, :n + 1].cpu().numpy(), lr)
+    finally:
+        tb.close()
+
+
+@pytest.mark.gpu
+def test_tband_refusals(torch_gpu):
+    torch = torch_gpu
+    n1, n2 = 300, 200
+    s1 = torch.from_numpy(nwhip.synth(1, n1)).cuda()
+    s2 = torch.from_numpy(nwhip.synth(2, n2)).cuda()
+    ctx = nwhip.Context(0)
+    tab = nwhip.Context.alloc_table(n1, n2)
+    feed = nwhip.Feed(n1, 0)
+    try:
+        with pytest.raises(nwhip.NwError) as e:  # a band below row 0 needs its feed
+            ctx.fill_tband(s1, s2, tab, row0=5)
+        assert e.value.status == nwhip.NW_ERR_ARG
+        with pytest.raises(nwhip.NwError) as e:  # band 0 has no feed
+            ctx.fill_tband(s1, s2, tab, row0=0, feed_in=feed.ptr)
+        assert e.value.status == nwhip.NW_ERR_ARG
+        with pytest.raises(nwhip.NwError) as e:  # tag 0 is never a launch tag
+            ctx.fill_tband(s1, s2, tab, tag=0)
+        assert e.value.status == nwhip.NW_ERR_ARG
+        big = nwhip.Context.alloc_table(n1, n2 + 64)
+        rows = nwhip.table_rows(n2)
+        with pytest.raises(nwhip.NwError) as e:  # misaligned table base (column 1 off its 256-B line)
+            ctx.fill_tband(s1, s2, big.view(-1)[1:1 + rows * big.shape[1]].view(rows, big.shape[1]))
+        assert e.value.status == nwhip.NW_ERR_ARG
+        with pytest.raises(nwhip.NwError) as e:  # Smith-Waterman is the single-table path's
+            lib_p = nwhip.params((1, -1, -1), mode=nwhip.MODE_SW)
+            st = nwhip.lib().nw_fill_tband_async(ctx._h, ctypes.c_void_p(s1.data_ptr()), n1,
+                                                 ctypes.c_void_p(s2.data_ptr()), n2, ctypes.byref(lib_p),
+                                                 ctypes.byref(nwhip.NwTBand(None, None, 1, 0, 0)),
+                                                 ctypes.c_void_p(tab.data_ptr()), tab.shape[1], None)
+            if st != nwhip.NW_OK:
+                raise nwhip.NwError(st, "nw_fill_tband_async")
+        assert e.value.status == nwhip.NW_ERR_UNSUPPORTED
+        torch.cuda.synchronize()
+        ctx.fill_tband(s1, s2, tab)  # and the context still works
+        torch.cuda.synchronize()
+        assert ctx.status() == nwhip.NW_OK
+        assert int(tab[n2, n1].item()) == oracle.score(nwhip.synth(1, n1), nwhip.synth(2, n2))
+    finally:
+        feed.free()
+        ctx.close()
