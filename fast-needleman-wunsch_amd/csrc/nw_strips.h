@@ -985,6 +985,11 @@ __device__ __forceinline__ void store_strip_tr(const FillArgs &A, char *__restri
             avail = (sa == kDone || sa == kDead) ? nx : min(sa - 63, nx);
             lds_order();  // ring reads after the counter that released them
         }
+        if (A.flags & 4) {  // debug: drain the ring without reading it (compute-pace probe)
+            lds_order();
+            ctr_store(mine, f + NS * BATCH);
+            continue;
+        }
         u32x4 v[NBLK][4];
 #pragma unroll
         for (int blk = 0; blk < NBLK; ++blk)

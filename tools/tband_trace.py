@@ -1,0 +1,50 @@
+"""Per-strip timeline of one horizontal-strip band fill (nw_fill_tband_async with
+the debug trace): the lag between adjacent strips at a quarter / the middle of
+the sweep (the hop), strip durations, feed waits -- s_memrealtime at 100 MHz."""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "fast-needleman-wunsch_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import nwhip  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--n1", type=int, default=524288)
+ap.add_argument("--n2", default="16384,65536")
+args = ap.parse_args()
+ctx = nwhip.Context(0)
+s1 = torch.from_numpy(nwhip.synth(1, args.n1)).cuda()
+for n2 in [int(x) for x in args.n2.split(",")]:
+    s2 = torch.from_numpy(nwhip.synth(2, n2)).cuda()
+    tab = nwhip.Context.alloc_table(args.n1, n2)
+    nstrips = -(-n2 // 256)
+    tr = torch.zeros(nstrips * 24, dtype=torch.int64, device="cuda")
+    ctx.fill_tband(s1, s2, tab, tag=1)
+    ctx.set_trace(tr)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    ctx.fill_tband(s1, s2, tab, tag=2)
+    e1.record()
+    torch.cuda.synchronize()
+    ctx.set_trace(None)
+    t = tr.view(nstrips, 24).cpu().numpy().astype(np.float64)
+    t0 = t[:, 0].min()
+    st, en = (t[:, 0] - t0) / 100.0, (t[:, 1] - t0) / 100.0
+    print(f"{args.n1}x{n2} strips={nstrips} ms={e0.elapsed_time(e1):.3f} span_us={en.max():.0f}")
+    for col, nm in ((4, "quarter"), (5, "mid")):
+        hop = np.diff(t[:, col]) / 100.0
+        print(f"  hop at {nm} (us): med {np.median(hop):.2f} p10 {np.percentile(hop, 10):.2f} "
+              f"p90 {np.percentile(hop, 90):.2f} max {hop.max():.1f}; first 8 {np.round(hop[:8], 2).tolist()}")
+    print(f"  start lag (us): med {np.median(np.diff(st)):.2f}; first 8 {np.round(np.diff(st)[:8], 2).tolist()}")
+    dur = en - st
+    print(f"  strip duration (us): first {dur[0]:.0f} med {np.median(dur):.0f} max {dur.max():.0f}; "
+          f"end of last {en[-1]:.0f}")
+    print(f"  feed waits / strip: med {np.median(t[:, 2]):.0f} max {t[:, 2].max():.0f}; wait us med "
+          f"{np.median(t[:, 3]) / 100:.0f} max {t[:, 3].max() / 100:.0f}; ring-space wait us (last wave) med "
+          f"{np.median(t[:, 12]) / 100:.0f}", flush=True)
+    del tab
+    torch.cuda.empty_cache()
