@@ -16,9 +16,14 @@ waves) with no host round trip and no copy engine, collective or
 stream-ordered gating on the data path.  torch.distributed (gloo) is the control plane
 only: handle exchange, the per-step barrier and the max-over-ranks timing.
 
-`LocalBands` runs P bands concurrently on ONE device (same kernels, same halo
-protocol, local instead of peer memory): an API for band-sized fills and the
-single-GPU parity vehicle for the multi-GPU path.
+The bench's main row-band leg sweeps each band in HORIZONTAL strips instead
+(nw_fill_tband_async: 256-row strips running along the columns, the halo a feed of
+one granule per column published 16 columns at a time), so that band r+1 starts a
+strip hop after band r rather than after band r's whole height.
+
+`LocalBands` / `LocalTBands` run P bands concurrently on ONE device (same kernels,
+same halo protocol, local instead of peer memory): an API for band-sized fills and
+the single-GPU parity vehicles for the multi-GPU path.
 """
 from __future__ import annotations
 
