@@ -230,6 +230,7 @@ __device__ __forceinline__ int32_t diag_plus_sub(uint32_t w, uint32_t apk, int32
 template <int C>
 struct Lanes {
     int32_t u[C];      // w = t - GAP*(i+j) of the lane's current row, column k
+    int32_t g[C];      // Smith-Waterman: sat0(t + GAP) of u[k] (the next row's "up + GAP")
     int32_t dg;        // w_diag of column 0 for the next step (= last step's w_left)
     int32_t rr;        // RAMP: row of this lane at the current step
     uint32_t apk;      // raw column characters of the lane, byte k = column k
@@ -381,6 +382,9 @@ __device__ __forceinline__ void run_iter(char *__restrict__ lds, int it, const u
 #endif
             int32_t diag = S.dg;
             S.dg = left;
+            // Smith-Waterman: the left neighbour's sat0(t + GAP) (one per step, column 0)
+            int32_t lg = 0;
+            if constexpr (is_sw<MODE>()) lg = (int32_t)__builtin_elementwise_sub_sat((uint32_t)left, (uint32_t)-gap);
             bool act = true;
             if constexpr (RAMP) {
                 S.rr += 1;
@@ -395,8 +399,13 @@ __device__ __forceinline__ void run_iter(char *__restrict__ lds, int it, const u
                 const int32_t d = diag_plus_sub<q, k, MODE>(w, S.apk, diag, msp, mmp);
                 int32_t x;
                 if constexpr (is_sw<MODE>()) {
-                    // t = max(0, t_diag + s, max(t_up, t_left) + GAP)
-                    x = max(max(d, max(S.u[k], left) + gap), 0);
+                    // t = max(0, t_diag + s, t_up + GAP, t_left + GAP)
+                    //   = max(t_diag + s, sat0(t_up + GAP), sat0(t_left + GAP))   (GAP <= 0)
+                    // the two saturated terms are >= 0 and carry the floor; sat0(t + GAP)
+                    // = usub_sat(t, -GAP) (cells are >= 0) is formed once per cell below
+                    // -- it is both the next row's up and the next column's left:
+                    // v_add (diag + s), v_max3, v_sub_u32 clamp = 3 VALU per cell
+                    x = max(max(d, S.g[k]), lg);
                 } else {
                     // w = max(w_diag + s - 2 GAP, w_up, w_left)  (w = t - GAP*(i+j))
                     x = max(max(d, S.u[k]), left);
@@ -406,6 +415,10 @@ __device__ __forceinline__ void run_iter(char *__restrict__ lds, int it, const u
                 if constexpr (RAMP) x = act ? x : S.u[k];
                 S.u[k] = x;
                 left = x;
+                if constexpr (is_sw<MODE>()) {
+                    lg = (int32_t)__builtin_elementwise_sub_sat((uint32_t)x, (uint32_t)-gap);
+                    S.g[k] = lg;
+                }
                 if constexpr (L::kGrp) {
                     gq[u & 3] = x;
                 } else {
@@ -546,6 +559,7 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
         const uint32_t a = (c >= 1 && c <= A.n1) ? (uint32_t)A.s1[c - 1] : 0u;
         S.apk |= a << (8 * k);
         S.u[k] = top[k] - (int32_t)((cl + k) * (int64_t)gw);  // w[0][c] = t[0][c] - GAP*c
+        S.g[k] = SW ? (int32_t)__builtin_elementwise_sub_sat((uint32_t)S.u[k], (uint32_t)-gap) : 0;
         if constexpr (MODE == SUB_PERM || MODE == SUB_PERM_SW) {
             const uint32_t x = (c >= 1 && c <= A.n1) ? (uint32_t)A.charmap[a] : 0xFFu;
             const uint32_t msb = (uint32_t)msp & 255u;
