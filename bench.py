@@ -60,11 +60,12 @@ def parse():
     ap.add_argument("--band-blocks", type=int, default=1,
                     help="N>1 row bands: blocks of rows per GPU, dealt round robin (1 = contiguous "
                          "mpi-horz bands; the block-cyclic alternate leg uses 2)")
-    ap.add_argument("--band-sweep", choices=["horizontal", "vertical"], default="horizontal",
+    ap.add_argument("--band-sweep", choices=["auto", "horizontal", "vertical"], default="auto",
                     help="N>1 contiguous row bands: swept in horizontal strips of 256 rows along the "
-                         "columns (default: band r+1 starts a strip hop after band r) or in the vertical "
-                         "strips of the single-table fill (band r+1 waits for band r's height); the other "
-                         "runs as an alternate leg")
+                         "columns (band r+1 starts a strip hop after band r) or in the vertical strips of "
+                         "the single-table fill (band r+1 waits for band r's height); auto: horizontal "
+                         "when a band holds 256 such strips (--band-rows >= 65536, the default); the "
+                         "other runs as an alternate leg")
     ap.add_argument("--kernel", type=int, default=0,
                     help="0 auto, 1 anti-diagonal strips, 2 row-scan panels (nw_params.kernel)")
     ap.add_argument("--col-width", type=int, default=65536,

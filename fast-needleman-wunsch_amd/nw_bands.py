@@ -525,6 +525,13 @@ def _sweep(args, partition: str, rank: int, world: int, dev: int, scheme, blocks
 CYCLE_ALT_BLOCKS = 2
 
 
+# A horizontal sweep runs its strips side by side along the whole width: a band of
+# fewer than 256 strips of 256 rows leaves CUs idle for the full n1-column sweep
+# (2 ranks sharing one GPU with 16384-row bands: 32.0 ms against 19.8 for the
+# vertical sweep, profiles/r03h_share2_bench.json), so `auto` sweeps vertically there.
+HSTRIP_ROWS, HSTRIP_CUS = 256, 256
+
+
 def legs_for(args) -> list:
     """[(name, partition, blocks per rank)] of a multi-GPU bench: the main one
     first (its value is the line's), then the alternates (--alt-partition).
@@ -539,7 +546,10 @@ def legs_for(args) -> list:
     if kernel == nwhip.KERNEL_PANELS:
         m = 1  # (no block-cyclic launch for the panel kernel)
     horiz_ok = kernel != nwhip.KERNEL_PANELS  # (horizontal strips: the (4, 1) strip kernel)
-    horiz = horiz_ok and getattr(args, "band_sweep", "horizontal") == "horizontal"
+    sweep = getattr(args, "band_sweep", "auto")
+    if sweep == "auto":  # horizontal once a band has a 256-row strip for every CU
+        sweep = "horizontal" if args.band_rows >= HSTRIP_ROWS * HSTRIP_CUS else "vertical"
+    horiz = horiz_ok and sweep == "horizontal"
     rows_h = ("rows_horizontal", "hrows", 1)
     rows_v = ("rows_contiguous", "rows", 1)
     rows_main = ("rows_cyclic", "rows", m) if m > 1 else rows_h if horiz else rows_v

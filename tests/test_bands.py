@@ -208,13 +208,14 @@ def test_two_process_bands_shared_gpu(torch_gpu, kernel, blocks, sweep):
     ({"kernel": 2}, ["rows_contiguous", "cols"]),
     ({"partition": "cols"}, ["cols", "rows_horizontal"]),
     ({"alt_partition": "none"}, ["rows_horizontal"]),
-    ({"band_rows": 704}, ["rows_horizontal", "rows_contiguous", "cols"]),
+    ({"band_rows": 704}, ["rows_contiguous", "rows_horizontal", "cols"]),
+    ({"band_rows": 704, "band_sweep": "horizontal"}, ["rows_horizontal", "rows_contiguous", "cols"]),
 ])
 def test_bench_legs(kw, want):
     """bench.py --gpus N: the row-band leg that is `value` (config 4: contiguous mpi-horz bands,
     horizontal strips unless --band-sweep vertical or --band-blocks m > 1) and the alternates."""
     import argparse
-    a = dict(partition="rows", kernel=0, band_blocks=1, band_sweep="horizontal", alt_partition=None,
+    a = dict(partition="rows", kernel=0, band_blocks=1, band_sweep="auto", alt_partition=None,
              band_rows=65536)
     a.update(kw)
     assert [name for name, _, _ in nw_bands.legs_for(argparse.Namespace(**a))] == want

@@ -10,7 +10,7 @@
 
 typedef unsigned v4 __attribute__((ext_vector_type(4)));
 
-template <int NS, int BATCH>
+template <int NS, int BATCH, bool NT = false>
 __global__ __launch_bounds__(64 * NS) void sweep(char *t, long pitchb, long nrows, int lag) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -26,28 +26,31 @@ __global__ __launch_bounds__(64 * NS) void sweep(char *t, long pitchb, long nrow
             long row = f + g + r0;
             if (f + g >= nrows) break;
             if (row >= nrows) row -= nrows;
-            *(v4 *)(base + row * pitchb) = v;
+            if constexpr (NT)
+                __builtin_nontemporal_store(v, (v4 *)(base + row * pitchb));
+            else
+                *(v4 *)(base + row * pitchb) = v;
             v.x += 1;
         }
     }
 }
 
-template <int NS, int BATCH>
+template <int NS, int BATCH, bool NT = false>
 static void run(char *t, long pitchb, long nrows, int lag) {
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
-    hipLaunchKernelGGL((sweep<NS, BATCH>), dim3(256), dim3(64 * NS), 0, 0, t, pitchb, nrows, lag);
+    hipLaunchKernelGGL((sweep<NS, BATCH, NT>), dim3(256), dim3(64 * NS), 0, 0, t, pitchb, nrows, lag);
     (void)hipEventRecord(e0, 0);
     for (int i = 0; i < 3; ++i)
-        hipLaunchKernelGGL((sweep<NS, BATCH>), dim3(256), dim3(64 * NS), 0, 0, t, pitchb, nrows, lag);
+        hipLaunchKernelGGL((sweep<NS, BATCH, NT>), dim3(256), dim3(64 * NS), 0, 0, t, pitchb, nrows, lag);
     (void)hipEventRecord(e1, 0);
     (void)hipEventSynchronize(e1);
     float ms = 0;
     (void)hipEventElapsedTime(&ms, e0, e1);
     ms /= 3;
     const double bytes = 262144.0 * 4096.0 / 4.0 * 4.0 * (double)nrows / 262144.0 * 256.0;  // 256 panels x 4 KB x rows
-    printf("store waves/CU=%d batch=%d lag=%d: %.2f ms  %.0f GB/s\n", NS, BATCH, lag, ms, bytes / (ms * 1e6));
+    printf("store waves/CU=%d batch=%d nt=%d lag=%d: %.2f ms  %.0f GB/s\n", NS, BATCH, (int)NT, lag, ms, bytes / (ms * 1e6));
 }
 
 int main(int argc, char **argv) {
@@ -80,6 +83,7 @@ int main(int argc, char **argv) {
             run<12, 8>(t, pitchb, nrows, lag);
         }
         run<8, 8>(t, pitchb, nrows, lag);
+        run<8, 8, true>(t, pitchb, nrows, lag);
     }
     (void)hipFree(t);
     return 0;
