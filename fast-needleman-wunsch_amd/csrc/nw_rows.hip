@@ -327,13 +327,28 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
     // ---- row characters: rowpack16[x + kQOff] = B[x .. x+15], B[y] = s2[y-1]
     // (mapped for PERM): entry e's 16 rows are one 16-byte entry, s_load'ed two
     // entries ahead into wd[e & 3]
-    const cu32 *rq = (const cu32 *)A.rowpack;
     uint32_t wd[4][4];
+#ifdef NW_ROWS_VLOAD
+    // a VECTOR load (every lane the same 16 bytes: one request), counted on vmcnt:
+    // an s_load shares lgkmcnt with the LDS and returns out of order, so every LDS
+    // wait issued while it is in flight is an lgkmcnt(0) that also waits for it
+    const char *rqv = (const char *)A.rowpack;
+    auto wload = [&](int32_t e, uint32_t (&o)[4]) {
+        int32_t z = 0;
+        asm volatile("" : "+v"(z));  // lane-varying to the compiler: no s_load
+        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+        const v4u v = *(const v4u *)(rqv + ((int64_t)e * kEnt + kQOff) * 16 + z);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = v[q];
+    };
+#else
+    const cu32 *rq = (const cu32 *)A.rowpack;
     auto wload = [&](int32_t e, uint32_t (&o)[4]) {
         const int64_t x0 = ((int64_t)__builtin_amdgcn_readfirstlane(e) * kEnt + kQOff) * 4;
 #pragma unroll
         for (int q = 0; q < 4; ++q) o[q] = rq[x0 + q];
     };
+#endif
 
     // ---- one row: x (row r-1) -> x (row r), lv = the left value of row r
 #ifdef NW_ROWS_CHAIN1
