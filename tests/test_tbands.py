@@ -3,6 +3,8 @@
 as 256-row strips along the columns, band r-1's last row fed to band r column by
 column.
 
+CPU (-m "not gpu"): the transposition contract the sweep rests on, with the
+oracle's band restatements.
 GPU (-m gpu): LocalTBands -- several bands concurrently on one device through
 the in-kernel feed hand-off -- bit-exact against the oracle's whole table (the
 serial.cpp:4-36 restatement) on ragged shapes, every scheme form, repeated
@@ -30,6 +32,28 @@ def torch_gpu():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch
+
+
+# ------------------------------------------------------------------ contract (CPU)
+@pytest.mark.parametrize("n1,n2,P", [(300, 200, 2), (129, 1000, 5), (7, 64, 3), (1000, 777, 8)])
+@pytest.mark.parametrize("scheme", [(1, 0, -1), (1, -1, -1), (2, -1, -2), (1, -1, 0)])
+def test_row_band_is_the_transposed_column_band(n1, n2, P, scheme):
+    """What nw_fill_tband_async computes: row band r of the table of (s1, s2) -- its row 0
+    the previous band's last row (mpi-horz.cpp:28-40) -- is the transpose of the column band
+    of the table of (s2, s1) over the same global indices with that row as its left column
+    (mpi-vert.cpp:4-109's contract), the scores being symmetric (serial.cpp:23-30).  Checked
+    with the oracle's own band restatements, band by band against the whole table."""
+    rng = np.random.default_rng(n1 + 7 * n2 + P)
+    s1 = rng.integers(1, 5, n1).astype(np.int8)
+    s2 = rng.integers(1, 5, n2).astype(np.int8)
+    full = oracle.fill(s1, s2, scheme)
+    np.testing.assert_array_equal(oracle.fill(s2, s1, scheme).T, full)
+    for r in range(P):
+        rows, start = oracle.band_layout(n2, P, r)
+        halo = full[start] if r > 0 else None
+        band_t = oracle.fill_colband(s2, s1, start, rows, halo, scheme)  # (n1 + 1) x rows
+        np.testing.assert_array_equal(band_t.T, full[start:start + rows], err_msg=f"band {r}")
+        np.testing.assert_array_equal(oracle.fill_band(s1, s2, P, r, halo, scheme), full[start:start + rows])
 
 
 def _check(torch, n1, n2, P, scheme, seed, alphabet=4):
