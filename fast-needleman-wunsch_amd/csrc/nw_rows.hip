@@ -38,8 +38,11 @@
 //   * A workgroup = NW compute waves (wave w: columns w*64C .. +64C-1 of the
 //     panel), kSPW store waves per compute wave (batches of its ring dealt
 //     round robin), a feeder-in and a feeder-out wave.  Compute waves touch
-//     only LDS (and s_load the row characters): every global-memory access of
-//     the hand-off sits in a wave of its own, whose stalls stall nobody else.
+//     only LDS (and load the row characters, 16 rows per 16-byte vector load:
+//     an s_load would share lgkmcnt with the LDS traffic and, returning out of
+//     order, turn every LDS wait behind it into a wait for it -- 256k: 46.0 ->
+//     44.5 ms): every global-memory access of the hand-off sits in a wave of its
+//     own, whose stalls stall nobody else.
 //   * Hand-off inside the panel: wave w reads wave w-1's last column straight
 //     out of w-1's ring; between panels: the feeder-out wave publishes the last
 //     compute wave's last column as {tag, value} granules as rows complete, the
@@ -325,10 +328,17 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
     };
 
     // ---- row characters: rowpack16[x + kQOff] = B[x .. x+15], B[y] = s2[y-1]
-    // (mapped for PERM): entry e's 16 rows are one 16-byte entry, s_load'ed two
+    // (mapped for PERM): entry e's 16 rows are one 16-byte entry, loaded kWPD
     // entries ahead into wd[e & 3]
     uint32_t wd[4][4];
-#ifdef NW_ROWS_VLOAD
+    // entries (16 rows each) the row characters are loaded ahead (at most 3: a ring of 4)
+#ifdef NW_ROWS_WPD
+    constexpr int kWPD = NW_ROWS_WPD;
+#else
+    constexpr int kWPD = 2;
+#endif
+    static_assert(kWPD >= 1 && kWPD <= 3, "");
+#ifndef NW_ROWS_SLOAD
     // a VECTOR load (every lane the same 16 bytes: one request), counted on vmcnt:
     // an s_load shares lgkmcnt with the LDS and returns out of order, so every LDS
     // wait issued while it is in flight is an lgkmcnt(0) that also waits for it
@@ -443,8 +453,8 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
     // (the initial x) goes into the ring without being computed.  The left
     // values of a group are loaded one group ahead.
     int32_t lvA[kG], lvB[kG];
-    wload(0, wd[0]);
-    wload(1, wd[1]);
+#pragma unroll
+    for (int e = 0; e < kWPD; ++e) wload(e, wd[e]);
     if (src != SRC_BOUND) ring_feed(kG);
     feed_load(0, lvA);
     if (src != SRC_BOUND) fbv = ctr_load(prod_written);
@@ -456,8 +466,7 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
             int32_t(&lv)[kG] = (g & 1) ? lvB : lvA;
             int32_t(&lvn)[kG] = (g & 1) ? lvA : lvB;
             ring_space(r0 + kG - kR);
-            // this group's substitution word (before anything else is queued on
-            // the LDS/SMEM counters: its s_load landed two entries ago)
+            // this group's substitution word (its load was issued kWPD entries ago)
             const uint32_t word = wd[(g >> 2) & 3][g & 3];
             uint32_t pks[C], tks[C];
 #pragma unroll
@@ -469,7 +478,7 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
                 tks[k] = 0u;
 #endif
             }
-            if constexpr ((g & 3) == 0) wload(r0 / kEnt + 2, wd[((g >> 2) + 2) & 3]);
+            if constexpr ((g & 3) == 0) wload(r0 / kEnt + kWPD, wd[((g >> 2) + kWPD) & 3]);
             // the next group's left values
             const int32_t rn = r0 + kG;
             if (rn < nrow_it) {
