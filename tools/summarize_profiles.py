@@ -24,7 +24,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 src, tag = sys.argv[1], sys.argv[2]
 dst = os.path.join(ROOT, "profiles")
 os.makedirs(dst, exist_ok=True)
-KERNEL = "nw_fill_strips"
+KERNEL = "nw_fill_"  # nw_fill_strips<...> or nw::rows::nw_fill_panels<...>
 
 
 def one(pattern):
@@ -67,9 +67,13 @@ fbytes = 2.0 * statistics.median(fe) * 1024.0
 shutil.copy(os.path.join(src, "bench.json"), os.path.join(dst, f"{tag}_bench.json"))
 tp = os.path.join(dst, "pmc_traffic.json")
 d = json.load(open(tp)) if os.path.exists(tp) else {}
-d[workload] = {"hbm_bytes_per_launch": wbytes + fbytes, "write_bytes": wbytes,
-               "fetch_bytes_x2": fbytes, "algorithmic_bytes": bench["roofline"]["bytes_per_launch"],
-               "round": tag, "rocprof_fill_ms_median": statistics.median(durs),
-               "bench_kernel_ms_avg": bench["roofline"]["kernel_ms_avg"]}
+key = f"{workload}:{bench['config'].get('kernel', 'strips')}"  # (bench.py pmc_traffic looks it up so)
+import datetime  # noqa: E402
+d[key] = {"hbm_bytes_per_launch": wbytes + fbytes, "write_bytes": wbytes,
+          "fetch_bytes_x2": fbytes, "algorithmic_bytes": bench["roofline"]["bytes_per_launch"],
+          "round": tag, "rocprof_fill_ms_median": statistics.median(durs),
+          "bench_kernel_ms_avg": bench["roofline"]["kernel_ms_avg"], "kernel_name": rows[0]["Kernel_Name"][:60],
+          "date": datetime.date.today().isoformat(),
+          "units": "WRITE_SIZE, FETCH_SIZE in KiB (x1024); FETCH doubled (gfx950 wide-read correction)"}
 json.dump(d, open(tp, "w"), indent=1, sort_keys=True)
-print(json.dumps(d[workload], indent=1))
+print(json.dumps(d[key], indent=1))
