@@ -481,10 +481,12 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
             if constexpr ((g & 3) == 0) wload(r0 / kEnt + kWPD, wd[((g >> 2) + kWPD) & 3]);
             // the next group's left values
             const int32_t rn = r0 + kG;
+#ifndef NW_ROWS_LATEFEED
             if (rn < nrow_it) {
                 if (src != SRC_BOUND) ring_feed(rn + kG);
                 feed_load(rn, lvn);
             }
+#endif
 #pragma unroll
             for (int u = 0; u < kG; ++u) {
                 if (!(g == 0 && u == 0) || trip != 0) row(word, pks, tks, u, lv[u]);
@@ -505,6 +507,15 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
             }
             lds_order();
             ctr_store(ctr, r0 + kG);  // rows written
+#ifdef NW_ROWS_LATEFEED
+            // the next group's left values once this group is out: a wave then trails
+            // its left neighbour by one group instead of two (the read's LDS latency
+            // is exposed at the next group's first row)
+            if (rn < nrow_it) {
+                if (src != SRC_BOUND) ring_feed(rn + kG);
+                feed_load(rn, lvn);
+            }
+#endif
         });
     }
     // every row is in the ring (or the panel is abandoned): release the store
