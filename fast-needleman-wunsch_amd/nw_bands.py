@@ -16,10 +16,11 @@ waves) with no host round trip and no copy engine, collective or
 stream-ordered gating on the data path.  torch.distributed (gloo) is the control plane
 only: handle exchange, the per-step barrier and the max-over-ranks timing.
 
-The bench's main row-band leg sweeps each band in HORIZONTAL strips instead
-(nw_fill_tband_async: 256-row strips running along the columns, the halo a feed of
-one granule per column published 16 columns at a time), so that band r+1 starts a
-strip hop after band r rather than after band r's whole height.
+An alternate leg sweeps each band in HORIZONTAL strips instead (nw_fill_tband_async:
+256-row strips running along the columns, the halo a feed of one granule per column
+published 16 columns at a time), so that band r+1 starts a strip hop after band r
+rather than after band r's whole height -- measured slower today because of how the
+feed is published.
 
 `LocalBands` / `LocalTBands` run P bands concurrently on ONE device (same kernels,
 same halo protocol, local instead of peer memory): an API for band-sized fills and
@@ -528,7 +529,7 @@ CYCLE_ALT_BLOCKS = 2
 # A horizontal sweep runs its strips side by side along the whole width: a band of
 # fewer than 256 strips of 256 rows leaves CUs idle for the full n1-column sweep
 # (2 ranks sharing one GPU with 16384-row bands: 32.0 ms against 19.8 for the
-# vertical sweep, profiles/r03h_share2_bench.json), so `auto` sweeps vertically there.
+# vertical sweep, profiles/r03h_share2_bench.json).
 HSTRIP_ROWS, HSTRIP_CUS = 256, 256
 
 
@@ -547,8 +548,12 @@ def legs_for(args) -> list:
         m = 1  # (no block-cyclic launch for the panel kernel)
     horiz_ok = kernel != nwhip.KERNEL_PANELS  # (horizontal strips: the (4, 1) strip kernel)
     sweep = getattr(args, "band_sweep", "auto")
-    if sweep == "auto":  # horizontal once a band has a 256-row strip for every CU
-        sweep = "horizontal" if args.band_rows >= HSTRIP_ROWS * HSTRIP_CUS else "vertical"
+    if sweep == "auto":
+        # vertical: measured ahead of the horizontal sweep whenever a band's top row
+        # arrives through a feed (2 bands of 524288 x 32768 on one GPU, in one process:
+        # 33.0 ms against 68.6, profiles/r03z_local_h.txt; 2 processes sharing it:
+        # 35.2 against 52.6, profiles/r03z_share2_h.json -- DESIGN.md section 5)
+        sweep = "vertical"
     horiz = horiz_ok and sweep == "horizontal"
     rows_h = ("rows_horizontal", "hrows", 1)
     rows_v = ("rows_contiguous", "rows", 1)
