@@ -63,7 +63,8 @@ def parse():
                     help="N>1 contiguous row bands: swept in horizontal strips of 256 rows along the "
                          "columns (band r+1 starts a strip hop after band r) or in the vertical strips of "
                          "the single-table fill (band r+1 waits for band r's height); auto = vertical "
-                         "(measured faster once the top row arrives through a feed, DESIGN.md section 5); "
+                         "(the horizontal sweep runs a band's leftover row as a second pass today, "
+                         "DESIGN.md section 5); "
                          "the other runs as an alternate leg")
     ap.add_argument("--kernel", type=int, default=0,
                     help="0 auto, 1 anti-diagonal strips, 2 row-scan panels (nw_params.kernel)")

@@ -578,6 +578,13 @@ void nw_band_layout(int64_t n2, int32_t nbands, int32_t r, int64_t *n_rows, int6
 // and system-scope coherence between agents is what fine-grained memory gives
 // (coarse-grained memory is only coherent at agent scope).
 static hipError_t alloc_link_buffer(void **p, size_t bytes) {
+    // NW_LINK_COARSE=1 (diagnostics, one device only): plain coarse-grained memory,
+    // to tell the feed's uncached-memory cost from the protocol's
+    static const bool coarse = [] {
+        const char *e = std::getenv("NW_LINK_COARSE");
+        return e != nullptr && e[0] == '1';
+    }();
+    if (coarse) return hipMalloc(p, bytes);
     return hipExtMallocWithFlags(p, bytes, hipDeviceMallocFinegrained);
 }
 

@@ -19,8 +19,8 @@ only: handle exchange, the per-step barrier and the max-over-ranks timing.
 An alternate leg sweeps each band in HORIZONTAL strips instead (nw_fill_tband_async:
 256-row strips running along the columns, the halo a feed of one granule per column
 published 16 columns at a time), so that band r+1 starts a strip hop after band r
-rather than after band r's whole height -- measured slower today because of how the
-feed is published.
+rather than after band r's whole height -- measured slower today: a band one row
+over a multiple of 256 rows runs that row as a second pass.
 
 `LocalBands` / `LocalTBands` run P bands concurrently on ONE device (same kernels,
 same halo protocol, local instead of peer memory): an API for band-sized fills and
@@ -549,10 +549,12 @@ def legs_for(args) -> list:
     horiz_ok = kernel != nwhip.KERNEL_PANELS  # (horizontal strips: the (4, 1) strip kernel)
     sweep = getattr(args, "band_sweep", "auto")
     if sweep == "auto":
-        # vertical: measured ahead of the horizontal sweep whenever a band's top row
-        # arrives through a feed (2 bands of 524288 x 32768 on one GPU, in one process:
-        # 33.0 ms against 68.6, profiles/r03z_local_h.txt; 2 processes sharing it:
-        # 35.2 against 52.6, profiles/r03z_share2_h.json -- DESIGN.md section 5)
+        # vertical: the mpi-horz partition gives bands after the first one row more
+        # than a multiple of 256 (the halo row; the last band the remainder), and the
+        # horizontal sweep runs that leftover row as a strip of its own -- a second full
+        # pass when the strips already fill the workers (2 bands of 524288 x 32768 on
+        # one GPU: 33.0 ms vertical against 68.6, profiles/r03z_local_h.txt; DESIGN.md
+        # section 5)
         sweep = "vertical"
     horiz = horiz_ok and sweep == "horizontal"
     rows_h = ("rows_horizontal", "hrows", 1)
