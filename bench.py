@@ -75,6 +75,10 @@ def parse():
                     help="N>1 rehearsal: every rank on device 0 (co-resident halves)")
     ap.add_argument("--workload", choices=["nw", "sw"], default="nw",
                     help="nw: the headline NW fill (config 3); sw: Smith-Waterman + traceback (config 5)")
+    ap.add_argument("--warmup-timeout-ms", type=int, default=5000,
+                    help="N>1: watchdog bound of every wait in the warmup launches (fail fast: a halo that "
+                         "never arrives ends the run in seconds, naming the band)")
+    ap.add_argument("--debug-withhold-rank", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-n", type=int, default=32768, help="CPU baseline sample side")
     args = ap.parse_args()

@@ -31,7 +31,7 @@ struct nw_ctx {
     uint8_t *meta = nullptr;   // charmap / nprof (nw::kMetaBytes)
     int32_t *scratch = nullptr;
     size_t scratch_cap = 0;
-    uint32_t *ctrl = nullptr;  // 4 words
+    uint32_t *ctrl = nullptr;  // nw::kCtrlWords: [0..7] per launch, [8..12] failure since the last status read
     uint32_t tagbase = 1;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int last_waves = 0;
@@ -48,6 +48,11 @@ struct nw_ctx {
     size_t tbscratch_cap = 0;
     int last_col0 = 0;
     int last_kernel = NW_KERNEL_STRIPS;
+    uint32_t last_failure[5] = {0, 0, 0, 0, 0};  // ctrl[8..12] as the last nw_ctx_status read them
+    uint64_t *look = nullptr;   // row-scan finisher look-back granules (nw_finish.hip)
+    size_t look_cap = 0;
+    uint32_t look_tag = 1;
+    int last_finish_rows = 0;   // rows the last horizontal-band launch left to the finisher
 };
 
 namespace {
@@ -291,7 +296,7 @@ int nw_ctx_create(int device, nw_ctx **out) {
     nw_ctx *c = new nw_ctx();
     c->device = device;
     c->cus = prop.multiProcessorCount;
-    if (hipMalloc(&c->ctrl, 32) != hipSuccess || hipMemset(c->ctrl, 0, 32) != hipSuccess ||
+    if (hipMalloc(&c->ctrl, nw::kCtrlWords * 4) != hipSuccess || hipMemset(c->ctrl, 0, nw::kCtrlWords * 4) != hipSuccess ||
         hipMalloc(&c->meta, nw::kMetaBytes) != hipSuccess || hipMemset(c->meta, 0, nw::kMetaBytes) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
         nw_ctx_destroy(c);
@@ -313,6 +318,7 @@ void nw_ctx_destroy(nw_ctx *c) {
     if (c->ops) (void)hipFree(c->ops);
     if (c->swinfo) (void)hipFree(c->swinfo);
     if (c->tbscratch) (void)hipFree(c->tbscratch);
+    if (c->look) (void)hipFree(c->look);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     delete c;
@@ -447,7 +453,8 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
     if ((st = grow((void **)&c->scratch, &c->scratch_cap, (size_t)s.waves * nw::kScratchWords * 4)) != NW_OK)
         return st;
 
-    NW_HIP_TRY(hipMemsetAsync(c->ctrl, 0, 32, (hipStream_t)stream));
+    // per-launch control words: reset, keeping a failure not yet reported (nw_link.hip nw_ctrl_reset)
+    if (nw::launch_ctrl_reset(c->ctrl, stream) != hipSuccess) return NW_ERR_HIP;
     const uint8_t *s1u = n1 > 0 ? (const uint8_t *)d_s1 : (const uint8_t *)c->ctrl;
     const uint8_t *s2u = n2 > 0 ? (const uint8_t *)d_s2 : (const uint8_t *)c->ctrl;
     // v_perm score tables when every substitution score minus 2*GAP fits int8
@@ -633,6 +640,18 @@ int nw_fill_tband_async(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t 
     // one the feed), n1 + 1 "rows" (the band's columns)
     Shape s = make_shape(R, n1, p->waves, 4, 1, c->cus, 1, false, NW_KERNEL_STRIPS);
     if (!shape_valid(s) || s.nstrips > INT32_MAX / 2 || s.nblocks > INT32_MAX / 2) return NW_ERR_ARG;
+    // Leftover rows: when the band's last strip would run ALONE as one more pass over
+    // all n1 columns (strips = k * workers + 1, e.g. config 4's last band: 65537 rows =
+    // 257 strips on 256 CUs), its rows are computed by the row-scan finisher after the
+    // strips instead (nw_finish.hip: one prefix-max scan per row across the width).
+    int64_t Rs = R, L = 0;
+    if (s.nstrips > s.waves && (s.nstrips - 1) % s.waves == 0 && !(p->flags & NW_FLAG_NO_FINISH) &&
+        !(p->flags & 1)) {
+        L = R - 256 * (s.nstrips - 1);
+        Rs = R - L;
+        s = make_shape(Rs, n1, p->waves, 4, 1, c->cus, 1, false, NW_KERNEL_STRIPS);
+        if (!shape_valid(s)) return NW_ERR_ARG;
+    }
     int st;
     const size_t gran_need = (size_t)(s.M * s.gstride) * sizeof(uint64_t);
     bool fresh = false;
@@ -649,7 +668,8 @@ int nw_fill_tband_async(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t 
     if ((st = grow((void **)&c->rowpack, &c->rowpack_cap, (size_t)qlen * 16)) != NW_OK) return st;
     if ((st = grow((void **)&c->scratch, &c->scratch_cap, (size_t)s.waves * nw::kScratchWords * 4)) != NW_OK)
         return st;
-    NW_HIP_TRY(hipMemsetAsync(c->ctrl, 0, 32, (hipStream_t)stream));
+    // per-launch control words: reset, keeping a failure not yet reported (nw_link.hip nw_ctrl_reset)
+    if (nw::launch_ctrl_reset(c->ctrl, stream) != hipSuccess) return NW_ERR_HIP;
     const bool perm_ok = fits_i8(p->match - 2 * p->gap) && fits_i8(p->mismatch - 2 * p->gap) &&
                          !(p->flags & NW_FLAG_NO_PROFILE);
     // lanes carry the band's row characters (charmap of s2_band), the row packs the columns' (s1)
@@ -663,11 +683,11 @@ int nw_fill_tband_async(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t 
     a.col_end = INT64_MAX;
     a.strip0 = 0;
     a.feed_in = tb->feed_in;
-    a.feed_out = tb->feed_out;
+    a.feed_out = L > 0 ? nullptr : tb->feed_out;  // (with a finisher, it publishes the last row)
     a.feed_tag = tb->tag;
     a.rowpack = c->rowpack;
     a.s1 = (const uint8_t *)d_s2 - tb->row0;  // s1[y - 1] = global row y's character
-    a.n1 = tb->row0 + R;                      // global last row
+    a.n1 = tb->row0 + Rs;                     // global last row the strips sweep
     a.n2 = n1;
     a.row0 = 0;
     a.col0 = tb->row0 + 1;                    // first swept global row
@@ -694,11 +714,44 @@ int nw_fill_tband_async(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t 
     a.hstride = n1 + 1;
     a.tr = 1;
     a.tr_y0 = tb->row0;
-    a.tr_pub = (int32_t)(R - 1 - 256 * (s.nstrips - 1));  // the last row's column in the last strip
+    a.tr_pub = (int32_t)(Rs - 1 - 256 * (s.nstrips - 1));  // the last row's column in the last strip
     if (nw::launch_fill(a, 4, 1, (int)s.waves, stream) != hipSuccess) return NW_ERR_HIP;
     if (nw::launch_tband_edges(tb->feed_in, d_t, pitch, n1, R + 1, p->gap, tb->row0, stream) != hipSuccess)
         return NW_ERR_HIP;
     c->tagbase += (uint32_t)s.nstrips + 1u;
+    c->last_finish_rows = (int)L;
+    if (L > 0) {
+        nw::FinishArgs f;
+        std::memset(&f, 0, sizeof f);
+        f.chunk_cols = nw::finish_chunk_cols(n1, c->cus);
+        f.nchunks = (int32_t)((n1 + f.chunk_cols - 1) / f.chunk_cols);
+        const size_t need = (size_t)L * (size_t)f.nchunks * sizeof(uint64_t);
+        bool fresh = false;
+        if ((st = grow((void **)&c->look, &c->look_cap, need, &fresh)) != NW_OK) return st;
+        if (fresh || (uint64_t)c->look_tag + 2u * (uint64_t)L + 2u >= 0xFFFFFFF0ull) {
+            NW_HIP_TRY(hipMemsetAsync(c->look, 0, c->look_cap, (hipStream_t)stream));
+            c->look_tag = 1;
+        }
+        f.table = d_t;
+        f.pitch = pitch;
+        f.s1 = (const uint8_t *)d_s1;
+        f.n1 = n1;
+        f.s2 = (const uint8_t *)d_s2;
+        f.li0 = Rs + 1;
+        f.nrows = L;
+        f.grow0 = tb->row0;
+        f.match = p->match;
+        f.mismatch = p->mismatch;
+        f.gap = p->gap;
+        f.look = c->look;
+        f.tag0 = c->look_tag;
+        f.ctrl = c->ctrl;
+        f.feed_out = tb->feed_out;
+        f.feed_tag = tb->tag;
+        f.timeout_ticks = a.timeout_ticks;
+        if (nw::launch_finish_rows(f, stream) != hipSuccess) return NW_ERR_HIP;
+        c->look_tag += 2u * (uint32_t)L + 2u;
+    }
     c->last_waves = (int)s.waves;
     c->last_strips = (int)s.nstrips;
     c->last_sub = 4;
@@ -770,9 +823,14 @@ int nw_link_alloc(int device, uint32_t **d_word) {
 }
 
 int nw_link_wait_async(uint32_t *d_word, uint32_t value, int32_t timeout_ms, void *stream) {
+    return nw_link_wait_ctx_async(nullptr, d_word, value, timeout_ms, stream);
+}
+
+int nw_link_wait_ctx_async(nw_ctx *c, uint32_t *d_word, uint32_t value, int32_t timeout_ms, void *stream) {
     if (!d_word || timeout_ms < 0) return NW_ERR_ARG;
     const uint64_t ticks = (uint64_t)(timeout_ms > 0 ? timeout_ms : 20000) * 100000ull;
-    return nw::launch_link_wait(d_word, value, ticks, stream) == hipSuccess ? NW_OK : NW_ERR_HIP;
+    return nw::launch_link_wait(d_word, value, ticks, c ? c->ctrl : nullptr, stream) == hipSuccess ? NW_OK
+                                                                                                  : NW_ERR_HIP;
 }
 
 int nw_link_signal_async(uint32_t *d_word, uint32_t value, void *stream) {
@@ -812,10 +870,28 @@ int nw_ipc_close_handle(void *d_ptr) {
 int nw_ctx_status(nw_ctx *c, void *stream) {
     if (!c) return NW_ERR_ARG;
     NW_HIP_TRY(hipSetDevice(c->device));
-    uint32_t w[4] = {0, 0, 0, 0};
+    uint32_t w[nw::kCtrlWords] = {};
     NW_HIP_TRY(hipMemcpyAsync(w, c->ctrl, sizeof w, hipMemcpyDeviceToHost, (hipStream_t)stream));
     NW_HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
-    return w[1] != 0 ? NW_ERR_TIMEOUT : NW_OK;
+    // the last launch's error word, or a failure any earlier launch (or a link wait)
+    // recorded since the last read -- read and cleared (nw_link.hip nw_ctrl_reset)
+    const bool failed = (w[1] != 0 && w[13] == 0) || w[8] != 0;
+    if (w[8] != 0 || w[12] != 0) {
+        for (int k = 0; k < 5; ++k) c->last_failure[k] = w[8 + k];
+    } else if (w[1] != 0 && w[13] == 0) {  // the last launch failed (not folded in yet)
+        c->last_failure[0] = w[1];
+        c->last_failure[1] = w[2];
+        c->last_failure[2] = w[3];
+        c->last_failure[3] = w[4];
+        c->last_failure[4] = 1;
+    }
+    if (failed) {
+        // clear the record and mark the last launch's words as read (ctrl[13])
+        static const uint32_t cleared[nw::kCtrlWords - 8] = {0, 0, 0, 0, 0, 1, 0, 0};
+        NW_HIP_TRY(hipMemcpyAsync(c->ctrl + 8, cleared, sizeof cleared, hipMemcpyHostToDevice, (hipStream_t)stream));
+        NW_HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    }
+    return failed ? NW_ERR_TIMEOUT : NW_OK;
 }
 
 int nw_fill_device(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *d_s2, int64_t n2,
@@ -1212,6 +1288,22 @@ int nw_debug_ctrl(nw_ctx *c, uint32_t *out8) {
     NW_HIP_TRY(hipSetDevice(c->device));
     NW_HIP_TRY(hipDeviceSynchronize());
     NW_HIP_TRY(hipMemcpy(out8, c->ctrl, 32, hipMemcpyDeviceToHost));
+    return NW_OK;
+}
+
+// Debug hook: the first failure recorded since the status before last was read
+// (code, site word, need, seen, failed launches) -- what nw_ctx_status cleared
+// when it last reported NW_ERR_TIMEOUT -- or, before any such read, the live words.
+int nw_debug_failure(nw_ctx *c, uint32_t *out5) {
+    if (!c || !out5) return NW_ERR_ARG;
+    NW_HIP_TRY(hipSetDevice(c->device));
+    NW_HIP_TRY(hipDeviceSynchronize());
+    uint32_t w[nw::kCtrlWords] = {};
+    NW_HIP_TRY(hipMemcpy(w, c->ctrl, sizeof w, hipMemcpyDeviceToHost));
+    if (w[8] != 0 || w[12] != 0)
+        for (int k = 0; k < 5; ++k) out5[k] = w[8 + k];
+    else
+        for (int k = 0; k < 5; ++k) out5[k] = c->last_failure[k];
     return NW_OK;
 }
 

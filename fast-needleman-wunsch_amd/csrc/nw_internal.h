@@ -129,8 +129,34 @@ int panel_lds_bytes(int c, int nwaves);
 int launch_panels(const FillArgs &a, int c, int nwaves, int grid, void *stream);
 // Band-to-band flow control (nw_link.hip): wait until word[0] >= value (word[1]
 // records a timeout), or store word[0] = value; one-lane kernels on `stream`
-int launch_link_wait(uint32_t *word, uint32_t value, uint64_t ticks, void *stream);
+int launch_link_wait(uint32_t *word, uint32_t value, uint64_t ticks, uint32_t *poison, void *stream);
+// reset a context's per-launch control words, keeping (and re-raising) its
+// recorded failure (nw_link.hip nw_ctrl_reset)
+int launch_ctrl_reset(uint32_t *ctrl, void *stream);
+constexpr int kCtrlWords = 16;
 int launch_link_signal(uint32_t *word, uint32_t value, void *stream);
+
+// Row-scan finisher (nw_finish.hip): rows li0 .. li0 + nrows - 1 of a row band
+// (local row 0 = global row grow0), every column 1..n1, each row a prefix
+// maximum in the w form with a decoupled look-back over column chunks.
+struct FinishArgs {
+    int32_t *table;            // band table, row-major (column 1 on a 256-byte line)
+    int64_t pitch;
+    const uint8_t *s1;         // column characters (n1)
+    int64_t n1;
+    const uint8_t *s2;         // the band's side characters: local row li uses s2[li - 1]
+    int64_t li0, nrows, grow0;
+    int32_t match, mismatch, gap;
+    uint64_t *look;            // [nrows][nchunks] look-back granules {tag, value}
+    uint32_t tag0;             // row r: aggregate tag0 + 2r, inclusive tag0 + 2r + 1 (unique per launch)
+    int32_t nchunks, chunk_cols;
+    uint32_t *ctrl;            // the context's control words: [1] error word, [6] chunk ticket
+    uint64_t *feed_out;        // the next band's feed (w form, one granule per column), or NULL
+    uint32_t feed_tag;
+    uint64_t timeout_ticks;
+};
+int finish_chunk_cols(int64_t n1, int cus);  // columns per chunk (256 threads x 8 or x 32)
+int launch_finish_rows(const FinishArgs &a, void *stream);
 int64_t rowpack_len(int32_t nblocks);  // 16-byte entries
 const char *kernel_variant();
 

@@ -451,67 +451,154 @@ def _sweep(args, partition: str, rank: int, world: int, dev: int, scheme, blocks
     waves = args.waves
     if args.share_gpu and waves == 0:
         waves = max(1, resident_waves(dev, sub, nc, kernel) // world)
+    # --debug-withhold-rank r: rank r never publishes its boundary (the fail-fast test)
+    withhold = getattr(args, "debug_withhold_rank", -1) == rank
+    warm_tmo = int(getattr(args, "warmup_timeout_ms", 5000))
+    try:
+        preflight(rank, world, stream, links_in, out_bufs, link_word, prod_word)
 
-    def launch(k: int, ev=None):
-        """Launch k (tag k >= 1) on this rank's stream, buffers k % 2."""
-        b = k % 2
-        if out_bufs is not None and k >= 3:
-            nwhip.link_wait(link_word.ptr, k - 2, stream)  # consumer done with launch k-2
-        if ev is not None:
-            ev[0].record(stream)
-        kw = dict(tag=k, scheme=scheme, waves=waves, stream=stream, substrips=sub, strip_waves=nc,
-                  kernel=kernel)
-        if cols:
-            ctx.fill_colband(s1, s2, table, world, rank, feed_in=links_in[b].ptr if links_in else None,
-                             feed_out=out_bufs[b] if out_bufs else None, **kw)
-        elif hrows:
-            ctx.fill_tband(s1, s2, table, row0=start, feed_in=links_in[b].ptr if links_in else None,
-                           feed_out=out_bufs[b] if out_bufs else None, tag=k, scheme=scheme, waves=waves,
-                           stream=stream)
-        elif cyc:
-            ctx.fill_band_cycle(s1, s2, h, table, halo_in=links_in[b].ptr, halo_out=out_bufs[b],
-                                hin_first=rank > 0, hout_shift=int(rank == world - 1), row0_max=start, **kw)
-        else:
-            ctx.fill_band(s1, s2, table, halo_in=links_in[b].ptr if links_in else None,
-                          halo_out=out_bufs[b] if out_bufs else None, row0=start, **kw)
-        if ev is not None:
-            ev[1].record(stream)
+        def launch(k: int, ev=None, timeout_ms: int = 0):
+            """Launch k (tag k >= 1) on this rank's stream, buffers k % 2."""
+            b = k % 2
+            if out_bufs is not None and k >= 3:
+                # consumer done with launch k-2; a wait that expires fails this context, so
+                # launch k gives up instead of rewriting the buffer the consumer still reads
+                nwhip.link_wait(link_word.ptr, k - 2, stream, timeout_ms=timeout_ms, ctx=ctx)
+            if ev is not None:
+                ev[0].record(stream)
+            hout = out_bufs[b] if out_bufs is not None and not withhold else None
+            kw = dict(tag=k, scheme=scheme, waves=waves, stream=stream, substrips=sub, strip_waves=nc,
+                      kernel=kernel, timeout_ms=timeout_ms)
+            if cols:
+                ctx.fill_colband(s1, s2, table, world, rank, feed_in=links_in[b].ptr if links_in else None,
+                                 feed_out=hout, **kw)
+            elif hrows:
+                ctx.fill_tband(s1, s2, table, row0=start, feed_in=links_in[b].ptr if links_in else None,
+                               feed_out=hout, tag=k, scheme=scheme, waves=waves, stream=stream,
+                               timeout_ms=timeout_ms)
+            elif cyc:
+                ctx.fill_band_cycle(s1, s2, h, table, halo_in=links_in[b].ptr, halo_out=hout,
+                                    hin_first=rank > 0, hout_shift=int(rank == world - 1), row0_max=start, **kw)
+            else:
+                ctx.fill_band(s1, s2, table, halo_in=links_in[b].ptr if links_in else None,
+                              halo_out=hout, row0=start, **kw)
+            if ev is not None:
+                ev[1].record(stream)
+            if prod_word is not None:
+                nwhip.link_signal(prod_word, k, stream)  # done reading launch k's buffer
+
+        # warmup: every rank starts together (barrier) and every wait is bounded by
+        # warm_tmo, so a halo / feed that never becomes visible (e.g. peer memory that
+        # behaves differently across devices) fails the run in seconds, naming the band
+        dist.barrier()
+        for k in range(1, args.warmup + 1):
+            launch(k, timeout_ms=warm_tmo)
+        torch.cuda.synchronize()
+        check_ranks(ctx, link_word, rank, world, f"{partition} warmup ({args.warmup} launches, "
+                    f"{warm_tmo} ms bound)")
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.steps)]
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i, e in enumerate(evs):
+            launch(args.warmup + 1 + i, e)
+        torch.cuda.synchronize()
+        dist.barrier()
+        wall = time.perf_counter() - t0
+        # any launch of the timed sweep that gave up (the record is sticky across launches)
+        status = ctx.status()
+        link_status = link_word.status() if link_word else 0
+        failure = ctx.debug_failure() if status != nwhip.NW_OK else None
+        kms = float(np.mean([a.elapsed_time(b) for a, b in evs])) if evs else 0.0
+        last = table[m - 1] if cyc else table
+        score = int(last[rows - 1, ncols - 1].item()) if rank == world - 1 else None
+        del last
+    finally:
+        torch.cuda.synchronize()
+        dist.barrier()
+        if out_bufs:
+            for x in out_bufs:
+                nwhip.ipc_close_handle(x)
         if prod_word is not None:
-            nwhip.link_signal(prod_word, k, stream)  # done reading launch k's buffer
+            nwhip.ipc_close_handle(prod_word)
+        dist.barrier()
+        for x in (links_in or []) + ([link_word] if link_word else []):
+            x.free()
+        ctx.close()
+        del table
+        torch.cuda.empty_cache()
+    return {"wall": wall, "status": status, "link_status": link_status, "failure": failure, "kms": kms,
+            "score": score, "n1": n1, "n2": n2, "shape": [sub, nc], "kernel": kernel, "rows": rows,
+            "start": start, "blocks": m, "block_rows": h}
 
-    for k in range(1, args.warmup + 1):
-        launch(k)
-    torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
+
+PING = 0x5A5A0000  # pre-flight marker (never a launch tag: tags count launches from 1)
+
+
+def preflight(rank: int, world: int, stream, links_in, out_bufs, link_word, prod_word, timeout_ms: int = 1000):
+    """Before any fill: every producer stores one word into its consumer's incoming
+    buffer (the halo / feed path, peer memory over xGMI) and every consumer stores
+    one into its producer's link word (the flow-control path); each side polls its
+    own copy with a `timeout_ms` bound (nw_link_wait).  A store that never becomes
+    visible fails every rank at once, naming the pair, instead of the first fill
+    waiting out its watchdog.  The marker words are cleared again before the
+    barrier that precedes the first launch."""
+    import torch
+    import torch.distributed as dist
     dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i, e in enumerate(evs):
-        launch(args.warmup + 1 + i, e)
-    torch.cuda.synchronize()
-    dist.barrier()
-    wall = time.perf_counter() - t0
-    status = ctx.status()
-    link_status = link_word.status() if link_word else 0
-    kms = float(np.mean([a.elapsed_time(b) for a, b in evs])) if evs else 0.0
-    last = table[m - 1] if cyc else table
-    score = int(last[rows - 1, ncols - 1].item()) if rank == world - 1 else None
-    dist.barrier()
-    if out_bufs:
-        for x in out_bufs:
-            nwhip.ipc_close_handle(x)
+    if out_bufs is not None:
+        nwhip.link_signal(out_bufs[0], PING | 1, stream)       # granule 0, value word of consumer's buffer 0
     if prod_word is not None:
-        nwhip.ipc_close_handle(prod_word)
+        nwhip.link_signal(prod_word + 8, PING | 2, stream)     # word 2 of the producer's link pair
+    fails = []
+    if links_in is not None:
+        nwhip.link_wait(links_in[0].ptr, PING | 1, stream, timeout_ms=timeout_ms)
+    if link_word is not None:
+        nwhip.link_wait(link_word.ptr + 8, PING | 2, stream, timeout_ms=timeout_ms)
+    torch.cuda.synchronize()
+    if links_in is not None and nwhip.link_status_at(links_in[0].ptr) != 0:
+        fails.append(f"rank {rank} never saw its producer's store into its incoming buffer")
+    if link_word is not None and nwhip.link_status_at(link_word.ptr + 8) != 0:
+        fails.append(f"rank {rank} never saw its consumer's store into its link word")
+    # clear the markers (granule 0 back to {tag 0, value 0}; link words 2, 3)
+    if links_in is not None:
+        for w in (0, 4):
+            nwhip.link_signal(links_in[0].ptr + w, 0, stream)
+    if link_word is not None:
+        for w in (8, 12):
+            nwhip.link_signal(link_word.ptr + w, 0, stream)
+    torch.cuda.synchronize()
+    allf = [None] * world
+    dist.all_gather_object(allf, fails)
+    bad = [f for fs in allf for f in fs]
+    if bad:
+        raise RuntimeError(f"pre-flight peer-store check failed ({timeout_ms} ms bound): " + "; ".join(bad))
     dist.barrier()
-    for x in (links_in or []) + ([link_word] if link_word else []):
-        x.free()
-    ctx.close()
-    del table, last
-    torch.cuda.empty_cache()
-    return {"wall": wall, "status": status, "link_status": link_status, "kms": kms, "score": score,
-            "n1": n1, "n2": n2, "shape": [sub, nc], "kernel": kernel, "rows": rows, "start": start,
-            "blocks": m, "block_rows": h}
+
+
+def check_ranks(ctx, link_word, rank: int, world: int, what: str) -> None:
+    """Every rank's fill status (sticky over the launches since the last check) and
+    link status, gathered; raise on every rank if any failed, naming the band, the
+    watchdog site and the recorded words."""
+    import torch.distributed as dist
+    st = ctx.status()
+    ls = link_word.status() if link_word else 0
+    mine = None
+    if st != nwhip.NW_OK or ls != 0:
+        code, site, need, seen, nfail = ctx.debug_failure()
+        mine = {"rank": rank, "status": nwhip.strerror(st) if st else "ok", "link_status": ls,
+                "code": code, "site": site >> 24, "wave": (site >> 16) & 0xFF, "need": need, "seen": seen,
+                "failed_launches": nfail, "debug_ctrl": ctx.debug_ctrl()}
+    allm = [None] * world
+    dist.all_gather_object(allm, mine)
+    bad = [m for m in allm if m is not None]
+    if bad:
+        raise RuntimeError(f"band fill failed during the {what}: " + "; ".join(
+            f"band {m['rank']}: {m['status']}, code {m['code']} (1 granule, 2 halo, 3 LDS counter, 4 link wait) "
+            f"at site {m['site']} wave {m['wave']}, needed {m['need']} saw {m['seen']}, "
+            f"{m['failed_launches']} failed launches, link status {m['link_status']}, debug_ctrl {m['debug_ctrl']}"
+            for m in bad))
 
 
 # Block-cyclic row bands on one GPU's share of config 4 (524288 x 65536), one launch
@@ -597,7 +684,10 @@ def run_bands(args) -> dict | None:
     dev = 0 if args.share_gpu else local % ndev
     torch.cuda.set_device(dev)
     if not dist.is_initialized():
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        # a bounded control plane: a rank that dies leaves the others' collectives
+        # failing within minutes rather than gloo's default half hour
+        import datetime
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=300))
     scheme = tuple(int(x) for x in args.scheme.split(","))
     legs = {}
     plan_ = legs_for(args)
@@ -621,13 +711,16 @@ def run_bands(args) -> dict | None:
                                       if k in alts]
         if plan_[0][1] in ("rows", "hrows"):  # the same table under every row partition
             out["rows_legs_agree"] = len(set(rows_legs)) == 1 if len(rows_legs) > 1 else None
+    # no value is published from a sweep whose watchdog or flow control tripped in
+    # any launch (the fill status is sticky over the launches of a sweep)
+    bad = [(p, [m["status"] for m in ms], [m["link_status"] for m in ms], [m["failure"] for m in ms])
+           for p, (_, ms) in legs.items() if any(m["status"] != 0 or m["link_status"] != 0 for m in ms)]
+    if bad:
+        raise RuntimeError(f"band status per rank (fill, link, first failure [code, site, need, seen, "
+                           f"launches]): {bad}")
     if cpu_baseline_fn is not None and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_fn(args.cpu_n, scheme)
     print(json.dumps(out), flush=True)
-    bad = [(p, [m["status"] for m in ms], [m["link_status"] for m in ms]) for p, (_, ms) in legs.items()
-           if any(m["status"] != 0 or m["link_status"] != 0 for m in ms)]
-    if bad:
-        raise RuntimeError(f"band status per rank (fill, link): {bad}")
     return out
 
 

@@ -36,7 +36,7 @@ EXPORTS = ["nw_params_default", "nw_strerror", "nw_version", "nw_fill", "nw_tabl
            "nw_debug_trace_words", "nw_colband_layout", "nw_feed_bytes", "nw_feed_alloc",
            "nw_fill_colband_async", "nw_link_alloc", "nw_link_wait_async", "nw_link_signal_async",
            "nw_link_status", "nw_host_warmup", "nw_host_release", "nw_halo_alloc_regions",
-           "nw_fill_band_cycle_async", "nw_fill_tband_async"]
+           "nw_fill_band_cycle_async", "nw_fill_tband_async", "nw_link_wait_ctx_async", "nw_debug_failure"]
 IPC_HANDLE_BYTES = 64
 
 
@@ -195,6 +195,9 @@ def lib() -> ctypes.CDLL:
                                       ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
     L.nw_link_alloc.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
     L.nw_link_wait_async.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int32, ctypes.c_void_p]
+    L.nw_link_wait_ctx_async.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int32,
+                                         ctypes.c_void_p]
+    L.nw_debug_failure.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32)]
     L.nw_link_signal_async.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
     L.nw_link_status.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32)]
     L.nw_host_warmup.argtypes = [ctypes.c_int]
@@ -267,7 +270,7 @@ def _seq(s) -> np.ndarray:
     return np.ascontiguousarray(np.asarray(s, dtype=np.int8))
 
 
-FLAG_TIMING_ONLY, FLAG_NO_PROFILE = 1, 2  # nw_params.flags (include/nw_hip.h)
+FLAG_TIMING_ONLY, FLAG_NO_PROFILE, FLAG_NO_FINISH = 1, 2, 4  # nw_params.flags (include/nw_hip.h)
 
 
 def fill(s1, s2, scheme=(1, 0, -1), waves: int = 0, device: int = -1, substrips: int = 0,
@@ -452,12 +455,24 @@ class Link(Halo):
         return int(out.value)
 
 
-def link_wait(ptr: int, value: int, stream, timeout_ms: int = 0) -> None:
-    """Stream-ordered wait until the link word at `ptr` is >= value (nw_link_wait_async)."""
-    st = lib().nw_link_wait_async(ctypes.c_void_p(ptr), int(value) & 0xFFFFFFFF, int(timeout_ms),
-                                  ctypes.c_void_p(stream.cuda_stream))
+def link_wait(ptr: int, value: int, stream, timeout_ms: int = 0, ctx: "Context | None" = None) -> None:
+    """Stream-ordered wait until the link word at `ptr` is >= value (nw_link_wait_async).
+    With `ctx` (nw_link_wait_ctx_async) a wait that gives up also fails that context:
+    its next fill gives up at once instead of rewriting a buffer still being read."""
+    st = lib().nw_link_wait_ctx_async(ctx._h if ctx is not None else None, ctypes.c_void_p(ptr),
+                                      int(value) & 0xFFFFFFFF, int(timeout_ms), ctypes.c_void_p(stream.cuda_stream))
     if st != NW_OK:
-        raise NwError(st, "nw_link_wait_async")
+        raise NwError(st, "nw_link_wait_ctx_async")
+
+
+def link_status_at(ptr: int) -> int:
+    """Word [1] of the word pair at `ptr` (nw_link_status): what a nw_link_wait on
+    `ptr` records when it gives up, 0 otherwise."""
+    out = ctypes.c_uint32()
+    st = lib().nw_link_status(ctypes.c_void_p(ptr), ctypes.byref(out))
+    if st != NW_OK:
+        raise NwError(st, "nw_link_status")
+    return int(out.value)
 
 
 def link_signal(ptr: int, value: int, stream) -> None:
@@ -662,14 +677,21 @@ class Context:
         the nw_fill_band contract (table: alloc_table(n1, len(d_s2_band)), row 0 =
         global row `row0` = the previous band's last row) with the band's rows swept
         as 256-row strips along the columns.  feed_in / feed_out: Feed(n1) buffers'
-        addresses (raw ints, e.g. peer memory from ipc_open_handle) or None at the ends."""
+        addresses (raw ints, e.g. peer memory from ipc_open_handle), int64 CUDA tensors
+        of feed_bytes(n1) / 8 granules, or None at the ends."""
         import torch
         n1, n2 = int(d_s1.numel()), int(d_s2_band.numel())
         assert table.dtype == torch.int32 and table.is_contiguous()
         assert table.shape[0] >= table_rows(n2) and table.shape[1] >= n1 + 1 and table.shape[1] % 64 == 0
+
+        def addr(x):
+            if x is None or isinstance(x, int):
+                return x
+            assert x.dtype == torch.int64 and x.numel() * 8 >= feed_bytes(n1)
+            return x.data_ptr()
         if stream is None:
             stream = torch.cuda.current_stream(table.device)
-        b = NwTBand(feed_in, feed_out, int(tag), 0, int(row0))
+        b = NwTBand(addr(feed_in), addr(feed_out), int(tag), 0, int(row0))
         p = params(scheme, waves, self.device, flags, 0, 0, timeout_ms)
         st = lib().nw_fill_tband_async(self._h, ctypes.c_void_p(d_s1.data_ptr() if n1 else 0), n1,
                                        ctypes.c_void_p(d_s2_band.data_ptr() if n2 else 0), n2, ctypes.byref(p),
@@ -709,7 +731,18 @@ class Context:
             raise NwError(st, "nw_debug_ctrl")
         return list(out)
 
+    def debug_failure(self) -> list[int]:
+        """The first failure recorded on this context (include/nw_hip.h nw_debug_failure):
+        [code, site word, need, seen, failed launches], pending or as the last status() cleared it."""
+        out = (ctypes.c_uint32 * 5)()
+        st = lib().nw_debug_failure(self._h, out)
+        if st != NW_OK:
+            raise NwError(st, "nw_debug_failure")
+        return list(out)
+
     def status(self, stream=None) -> int:
+        """NW_ERR_TIMEOUT if any launch on this context since the last call gave up
+        (nw_ctx_status: read and cleared), else NW_OK."""
         import torch
         if stream is None:
             stream = torch.cuda.current_stream()

@@ -49,8 +49,11 @@ enum { NW_MODE_NW = 0, NW_MODE_SW = 1 };
 /* nw_params.flags (0 = normal fill) */
 enum {
     NW_FLAG_TIMING_ONLY = 1, /* table stores go to a scratch tile (kernel timing only) */
-    NW_FLAG_NO_PROFILE = 2   /* substitution by byte compares instead of the per-lane
+    NW_FLAG_NO_PROFILE = 2,  /* substitution by byte compares instead of the per-lane
                                 v_perm score tables */
+    NW_FLAG_NO_FINISH = 4    /* nw_fill_tband_async: sweep every row in strips, also a
+                                last strip that runs alone as one more pass (default:
+                                such rows go to the row-scan finisher) */
 };
 
 /* nw_params.kernel: which gfx950 kernel family fills the table.  Both compute
@@ -420,24 +423,38 @@ int nw_ipc_close_handle(void *d_ptr);
  * nw_link_wait_async: stream-ordered wait until word[0] >= value (wrapping
  *   compare); after timeout_ms (0 = 20000) it gives up and records value in
  *   word[1].
+ * nw_link_wait_ctx_async: the same, and a wait that gives up also records the
+ *   failure in ctx (code 4): ctx's next fill then gives up at once, without
+ *   publishing into the buffer its consumer has not released, and nw_ctx_status
+ *   reports NW_ERR_TIMEOUT.
  * nw_link_signal_async: stream-ordered word[0] = value (word may be peer memory).
  * nw_link_status: word[1] (0 = no wait gave up), read synchronously. */
 int nw_link_alloc(int device, uint32_t **d_word);
 int nw_link_wait_async(uint32_t *d_word, uint32_t value, int32_t timeout_ms, void *stream);
+int nw_link_wait_ctx_async(nw_ctx *ctx, uint32_t *d_word, uint32_t value, int32_t timeout_ms, void *stream);
 int nw_link_signal_async(uint32_t *d_word, uint32_t value, void *stream);
 int nw_link_status(const uint32_t *d_word, uint32_t *out);
 
-/* Check the in-kernel watchdog word of the last launch (syncs the stream). */
+/* NW_ERR_TIMEOUT if ANY launch on ctx since the previous call gave up (an
+ * in-kernel watchdog, or a nw_link_wait_ctx_async that expired), else NW_OK;
+ * syncs the stream and clears the record.  Until it is read, a recorded failure
+ * makes every later launch on ctx give up at once (a back-to-back sweep stops
+ * at its first failure instead of waiting out one watchdog per launch). */
 int nw_ctx_status(nw_ctx *ctx, void *stream);
 
 /* Debug hooks (diagnosis, not needed for fills).
  * nw_debug_ctrl: the 8 control words of the context's last launch: [0] strip
  *   ticket, [1] error code (0 ok; 1 hand-off granule wait, 2 halo wait, 3 LDS
  *   counter wait expired), [2] site << 24 | wave << 16 | address bits, [3] the
- *   value the wait needed, [4] the value it last saw.  Syncs the device.
+ *   value the wait needed, [4] the value it last saw.  Syncs the device.  (A
+ *   launch that a recorded failure made give up carries that failure's words.)
+ * nw_debug_failure: the first failure recorded on ctx -- code (1 granule wait,
+ *   2 halo wait, 3 LDS counter, 4 link wait), site word, need, seen, and the
+ *   number of failed launches -- pending, or as the last nw_ctx_status cleared it.
  * nw_debug_set_trace: per-strip timeline buffer (device memory of at least
  *   strips * nw_debug_trace_words() uint64), NULL = off. */
 int nw_debug_ctrl(nw_ctx *ctx, uint32_t *out8);
+int nw_debug_failure(nw_ctx *ctx, uint32_t *out5);
 int nw_debug_set_trace(nw_ctx *ctx, void *d_trace);
 int32_t nw_debug_trace_words(void);
 

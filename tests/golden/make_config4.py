@@ -1,0 +1,93 @@
+#!/usr/bin/env python3
+"""Golden vectors for BASELINE config 4's per-rank row bands: the 524288 x 524288
+synthetic table (s1 = synth(1), s2 = synth(2), scheme (1, 0, -1) as shipped)
+split into 8 contiguous row bands exactly as src/mpi/mpi-horz-driver.cpp:31-32
+lays them out (oracle.band_layout; band r > 0 starts at its halo row 65536 r - 1,
+the last band takes the remainder row).
+
+From the pinned linear-memory oracle (oracle/nw_oracle.c nw_oracle_score /
+nw_oracle_rows, restating src/serial/serial.cpp:21-33), written to
+tests/golden/config4_524288_shipped.npz:
+  score          t[n2][n1] = the score mpi-horz-driver.cpp:88-90 prints (214685)
+  rows, first, d every band-boundary row (65536 r - 1 and 65536 r, r = 1..7: each
+                 band's halo row and its first computed row; 65536 r - 1 is also
+                 band r-1's last row), row 1, row n2, and seeded rows inside bands 3
+                 and 7 -- whole rows, column 0 + int8 differences along the row
+  last_col       t[0..n2][n1], delta-encoded
+  cs_bands       the bands whose every row has checksums: 3 and 7
+  row_sum_<r>,   (sum, (j+1)-weighted sum) mod 2^64 of every row of band r
+  row_wsum_<r>   (its halo row included), delta-encoded
+tests/test_config4.py decodes it; a GPU test fills one rank's band alone on one
+MI355X with its halo row pre-published from this fixture.
+"""
+import os
+import sys
+import time
+from concurrent.futures import ProcessPoolExecutor
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+N, P, SCHEME = 524288, 8, (1, 0, -1)
+CS_BANDS = (3, 7)
+OUT = os.path.join(HERE, "config4_524288_shipped.npz")
+
+
+def encode(a):
+    a = np.asarray(a)
+    with np.errstate(over="ignore"):
+        return np.concatenate([a[:1], np.diff(a)])
+
+
+def pick_rows():
+    import oracle
+    want = {1, N}
+    for r in range(1, P):
+        _, st = oracle.band_layout(N, P, r)
+        want |= {st, st + 1}
+    rng = np.random.default_rng(4)
+    for r in CS_BANDS:
+        nr, st = oracle.band_layout(N, P, r)
+        want |= {int(x) for x in rng.integers(st + 2, st + nr, 6)}
+    return np.array(sorted(want), dtype=np.int64)
+
+
+def sums_job():
+    import oracle
+    t0 = time.time()
+    sc, lr, lc, rs, rw = oracle.score(oracle.synth(1, N), oracle.synth(2, N), SCHEME, want_rows=True)
+    return sc, lr, lc, rs, rw, time.time() - t0
+
+
+def rows_job():
+    import oracle
+    t0 = time.time()
+    rows = pick_rows()
+    t = oracle.rows(oracle.synth(1, N), oracle.synth(2, N), SCHEME, rows)
+    return rows, t, time.time() - t0
+
+
+def main():
+    import oracle
+    with ProcessPoolExecutor(max_workers=2) as ex:
+        fs, fr = ex.submit(sums_job), ex.submit(rows_job)
+        sc, lr, lc, rs, rw, dt1 = fs.result()
+        rows, t, dt2 = fr.result()
+    assert t[-1, -1] == sc and np.array_equal(t[-1], lr)
+    d = np.diff(t, axis=1)
+    assert np.abs(d).max() < 128
+    out = dict(score=np.int64(sc), rows=rows, first=t[:, 0].copy(), d=d.astype(np.int8),
+               last_col=encode(lc), cs_bands=np.array(CS_BANDS, np.int64))
+    for r in CS_BANDS:
+        nr, st = oracle.band_layout(N, P, r)
+        out[f"row_sum_{r}"] = encode(rs[st:st + nr])
+        out[f"row_wsum_{r}"] = encode(rw[st:st + nr])
+    np.savez_compressed(OUT, **out)
+    print(f"score {sc}; {rows.size} rows; sums {dt1:.0f}s, rows {dt2:.0f}s", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -201,6 +201,33 @@ def test_two_process_bands_shared_gpu(torch_gpu, kernel, blocks, sweep):
     assert alts["cols"]["config"]["n1"] == 2 * width
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("nproc,withhold,extra", [
+    (2, 0, ["--band-sweep", "vertical"]), (2, 0, ["--band-sweep", "horizontal"]),
+    (3, 1, ["--band-sweep", "vertical"]), (2, 0, ["--partition", "cols"])])
+def test_withheld_producer_fails_fast(torch_gpu, nproc, withhold, extra):
+    """the driver's multi-GPU run must fail fast.  A producer that never
+    publishes its boundary (--debug-withhold-rank) makes its consumer's warmup wait
+    give up after --warmup-timeout-ms; every rank then exits non-zero within seconds,
+    naming the band, the watchdog site and the control words, and no JSON line is
+    printed.  (The pre-flight peer-store ping passes: the buffers are mapped.)"""
+    import time
+    env = dict(os.environ, PYTHONPATH=PKG)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(ROOT, "bench.py"), "--gpus", str(nproc), "--steps", "3", "--warmup", "2",
+           "--share-gpu", "--band-rows", "704", "--band-cols", "4113", "--col-width", "1500", "--col-rows", "1300",
+           "--alt-partition", "none", "--no-cpu-baseline", "--warmup-timeout-ms", "2000",
+           "--debug-withhold-rank", str(withhold)] + extra
+    t0 = time.time()
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    dt = time.time() - t0
+    assert out.returncode != 0
+    assert dt < 60, f"took {dt:.0f} s"
+    assert not [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert f"band {withhold + 1}: " in out.stderr and "warmup" in out.stderr, out.stderr[-3000:]
+
+
 @pytest.mark.parametrize("kw,want", [
     ({}, ["rows_contiguous", "rows_horizontal", "rows_cyclic", "cols"]),
     ({"band_sweep": "horizontal"}, ["rows_horizontal", "rows_contiguous", "rows_cyclic", "cols"]),

@@ -48,14 +48,14 @@ def alloc_aligned_table(torch, n1, n2):
 
 
 def device_fill(torch, ctx, s1, s2, scheme=(1, 0, -1), waves=0, substrips=0, strip_waves=0,
-                col0=1):
+                col0=1, kernel=nwhip.KERNEL_AUTO):
     d1 = torch.from_numpy(np.ascontiguousarray(s1)).cuda()
     d2 = torch.from_numpy(np.ascontiguousarray(s2)).cuda()
     if col0 == 1:
         tab = nwhip.Context.alloc_table(s1.size, s2.size)
     else:
         tab = alloc_aligned_table(torch, s1.size, s2.size)
-    r = ctx.fill(d1, d2, tab, scheme, waves=waves, substrips=substrips, strip_waves=strip_waves)
+    r = ctx.fill(d1, d2, tab, scheme, waves=waves, substrips=substrips, strip_waves=strip_waves, kernel=kernel)
     assert r.status == 0
     return tab, r
 
@@ -234,6 +234,78 @@ def test_watchdog_reports_timeout(torch, strip):
         assert r.status == 0
         np.testing.assert_array_equal(tab2[:rows + 1, :n1 + 1].cpu().numpy(), oracle.fill(s1, s2))
     finally:
+        c.close()
+
+
+@pytest.mark.parametrize("kernel", [nwhip.KERNEL_STRIPS, nwhip.KERNEL_PANELS])
+def test_failure_is_sticky_across_launches(torch, kernel):
+    """a watchdog trip in launch k of a back-to-back sweep must survive
+    the launches after it.  Launch 1 waits for a halo that never comes (200 ms
+    bound); launches 2 and 3 are enqueued behind it with no status read between:
+    they start poisoned and give up at once (no 20 s wait each, no halo published),
+    and the one status read afterwards reports NW_ERR_TIMEOUT with launch 1's
+    diagnosis (code 2 halo wait, tag 7) and 3 failed launches.  The read clears the
+    record: the next fill is exact."""
+    import time
+    c = nwhip.Context(0)
+    try:
+        n1, rows = 64 * 40 + 5, 300
+        s1, s2 = nwhip.synth(3, n1), nwhip.synth(4, rows)
+        d1, d2 = torch.from_numpy(s1).cuda(), torch.from_numpy(s2).cuda()
+        tab = nwhip.Context.alloc_table(n1, rows)
+        halo = torch.zeros(n1 + 1, dtype=torch.int64, device="cuda")  # tag 0 everywhere
+        out = torch.zeros(n1 + 1, dtype=torch.int64, device="cuda")
+        t0 = time.time()
+        c.fill_band(d1, d2, tab, halo_in=halo, tag=7, timeout_ms=200, kernel=kernel)
+        torch.cuda.synchronize()
+        t1 = time.time()
+        for tag in (8, 9):  # a normal band fill (no halo in), publishing its last row
+            c.fill_band(d1, d2, tab, halo_out=out, tag=tag, timeout_ms=20000, kernel=kernel)
+        torch.cuda.synchronize()
+        assert time.time() - t1 < 5, "poisoned launches must give up at once"
+        assert t1 - t0 < 30
+        assert int((out >> 32).count_nonzero()) == 0, "a poisoned launch published its halo"
+        code, site, need, seen, nfail = c.debug_failure()
+        # strips: the halo wait at a strip's start (code 2, site 4, the tag); panels:
+        # the feeder-in wave's granule wait on the halo (code 1, site 13)
+        want = (2, 4) if kernel == nwhip.KERNEL_STRIPS else (1, 13)
+        assert (code, site >> 24) == want and nfail >= 2
+        if kernel == nwhip.KERNEL_STRIPS:
+            assert need == 7
+        assert c.status() == nwhip.NW_ERR_TIMEOUT
+        assert c.debug_failure()[0] == want[0]  # as the status read cleared it
+        assert c.status() == nwhip.NW_OK  # cleared
+        tab2, r = device_fill(torch, c, s1, s2, (1, 0, -1), kernel=kernel)
+        assert r.status == 0
+        np.testing.assert_array_equal(tab2[:rows + 1, :n1 + 1].cpu().numpy(), oracle.fill(s1, s2))
+    finally:
+        c.close()
+
+
+def test_link_wait_timeout_poisons_the_producer(torch):
+    """a producer whose consumer never releases a buffer (its link word
+    never reaches the launch) must not rewrite that buffer.  The expired
+    nw_link_wait_ctx_async records code 4 in the producer's context, so its next
+    band fill publishes nothing, and the context's status reports the failure."""
+    c = nwhip.Context(0)
+    link = nwhip.Link(0)
+    try:
+        n1, rows = 64 * 40 + 5, 300
+        d1 = torch.from_numpy(nwhip.synth(3, n1)).cuda()
+        d2 = torch.from_numpy(nwhip.synth(4, rows)).cuda()
+        tab = nwhip.Context.alloc_table(n1, rows)
+        out = torch.zeros(n1 + 1, dtype=torch.int64, device="cuda")
+        st = torch.cuda.current_stream()
+        nwhip.link_wait(link.ptr, 5, st, timeout_ms=100, ctx=c)  # nobody signals 5
+        c.fill_band(d1, d2, tab, halo_out=out, tag=3)
+        torch.cuda.synchronize()
+        assert link.status() == 5
+        assert int((out >> 32).count_nonzero()) == 0
+        code, site, need, seen, nfail = c.debug_failure()
+        assert (code, site >> 24, need, seen) == (4, 20, 5, 0)
+        assert c.status() == nwhip.NW_ERR_TIMEOUT and c.status() == nwhip.NW_OK
+    finally:
+        link.free()
         c.close()
 
 

@@ -175,3 +175,83 @@ def test_tband_refusals(torch_gpu):
     finally:
         feed.free()
         ctx.close()
+
+
+# ------------------------------------------------------------------ the row-scan finisher
+def _tband_chain(torch, s1, s2, P, scheme, waves, flags=0, row_split=None):
+    """P bands of the (s1, s2) table, each filled by its own nw_fill_tband_async with
+    `waves` workers, one after the other on one stream (band r's feed_out is band r+1's
+    feed_in).  Returns (band tables, [published feed of band r]) as numpy."""
+    n1, n2 = s1.size, s2.size
+    ctx = nwhip.Context(0)
+    d1 = torch.from_numpy(s1).cuda()
+    fsize = nwhip.feed_bytes(n1) // 8
+    feeds = [torch.zeros(fsize, dtype=torch.int64, device="cuda") for _ in range(P - 1)]
+    out, pub = [], []
+    try:
+        for r in range(P):
+            rows, start = oracle.band_layout(n2, P, r) if row_split is None else row_split[r]
+            tab = nwhip.Context.alloc_table(n1, rows - 1)
+            d2 = torch.from_numpy(s2[start:start + rows - 1].copy()).cuda()
+            ctx.fill_tband(d1, d2, tab, row0=start, feed_in=feeds[r - 1] if r > 0 else None,
+                           feed_out=feeds[r] if r + 1 < P else None, tag=5, scheme=scheme, waves=waves,
+                           flags=flags)
+            torch.cuda.synchronize()
+            assert ctx.status() == nwhip.NW_OK, f"band {r}: {ctx.debug_failure()}"
+            out.append(tab[:rows, :n1 + 1].cpu().numpy())
+            if r + 1 < P:
+                pub.append(feeds[r].cpu().numpy()[:n1 + 1])
+        return out, pub
+    finally:
+        ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n1", [1, 100, 2047, 2048, 2049, 5000])
+@pytest.mark.parametrize("waves,extra", [(1, 1), (2, 7), (2, 64), (3, 200), (1, 256), (4, 129)])
+def test_tband_finisher_rows(torch_gpu, n1, waves, extra):
+    """A band whose last strip would run alone as one more pass over all columns
+    (strips = k * workers + 1) leaves that strip's rows (`extra` of them) to the
+    row-scan finisher (nw_finish.hip): one prefix-max scan per row across the width,
+    chunks of 2048 columns chained by a decoupled look-back.  Bit-exact against the
+    oracle under three scheme forms, with and without a halo row above it, and the
+    feed it publishes for the next band equals its last row (w form)."""
+    torch = torch_gpu
+    R = 256 * waves + extra  # strips = waves + 1
+    rng = np.random.default_rng(n1 * 7 + waves * 131 + extra)
+    s1 = rng.integers(1, 5, n1).astype(np.int8)
+    s2 = rng.integers(1, 5, 2 * R + 1).astype(np.int8)
+    for scheme in [(1, 0, -1), (1, -1, -1), (2, -1, -2)]:
+        full = oracle.fill(s1, s2, scheme)
+        split = [(R + 1, 0), (R + 1, R)]  # two bands of R computed rows each, the second below a halo
+        tabs, pub = _tband_chain(torch, s1, s2, 2, scheme, waves, row_split=split)
+        for r, (rows, start) in enumerate(split):
+            np.testing.assert_array_equal(tabs[r], full[start:start + rows], err_msg=f"band {r} {scheme}")
+        gap = scheme[2]
+        vals = (pub[0] & 0xFFFFFFFF).astype(np.uint32).view(np.int32).astype(np.int64)
+        np.testing.assert_array_equal(vals + gap * (np.arange(n1 + 1) + R), full[R], err_msg=f"feed {scheme}")
+        assert np.all((pub[0] >> 32) == 5)
+
+
+@pytest.mark.gpu
+def test_tband_finisher_matches_full_pass(torch_gpu):
+    """The finisher's rows equal the strip kernel's own second pass (NW_FLAG_NO_FINISH)."""
+    torch = torch_gpu
+    n1, waves = 3000, 2
+    R = 256 * waves * 2 + 3  # strips = 2 * waves + 1
+    rng = np.random.default_rng(9)
+    s1 = rng.integers(1, 5, n1).astype(np.int8)
+    s2 = rng.integers(1, 5, R).astype(np.int8)
+    a, _ = _tband_chain(torch, s1, s2, 1, (1, 0, -1), waves)
+    b, _ = _tband_chain(torch, s1, s2, 1, (1, 0, -1), waves, flags=nwhip.FLAG_NO_FINISH)
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[0], oracle.fill(s1, s2))
+
+
+@pytest.mark.gpu
+def test_local_tbands_leftover_row(torch_gpu):
+    """The mpi-horz partition's leftover row (bands after the first carry their halo
+    row, the last one the remainder): 2 bands sharing the GPU (each 1/2 of the workers),
+    the second sweeping 32769 rows = 129 strips on 128 workers -- the configuration that
+    ran a second full pass before the finisher."""
+    _check(torch_gpu, 300, 65537, 2, (1, 0, -1), 3)
