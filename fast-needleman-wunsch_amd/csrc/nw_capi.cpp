@@ -584,14 +584,24 @@ void nw_band_layout(int64_t n2, int32_t nbands, int32_t r, int64_t *n_rows, int6
 // system-scope stores while this GPU's kernel polls it with system-scope loads,
 // and system-scope coherence between agents is what fine-grained memory gives
 // (coarse-grained memory is only coherent at agent scope).
-static hipError_t alloc_link_buffer(void **p, size_t bytes) {
-    // NW_LINK_COARSE=1 (diagnostics, one device only): plain coarse-grained memory,
-    // to tell the feed's uncached-memory cost from the protocol's
+// NW_LINK_COARSE=1 (diagnostics, one device and one process only): plain
+// coarse-grained memory, to tell the feed's uncached-memory cost from the
+// protocol's.  Coarse-grained memory is coherent at agent
+// scope only, so such a buffer is never exported (nw_ipc_get_handle refuses).
+static bool link_coarse() {
     static const bool coarse = [] {
         const char *e = std::getenv("NW_LINK_COARSE");
-        return e != nullptr && e[0] == '1';
+        const bool on = e != nullptr && e[0] == '1';
+        if (on)
+            std::fprintf(stderr, "libnwhip: NW_LINK_COARSE=1: halo / feed / link buffers are coarse-grained "
+                                 "(single-device diagnostics; IPC export refused)\n");
+        return on;
     }();
-    if (coarse) return hipMalloc(p, bytes);
+    return coarse;
+}
+
+static hipError_t alloc_link_buffer(void **p, size_t bytes) {
+    if (link_coarse()) return hipMalloc(p, bytes);
     return hipExtMallocWithFlags(p, bytes, hipDeviceMallocFinegrained);
 }
 
@@ -846,6 +856,7 @@ int nw_link_status(const uint32_t *d_word, uint32_t *out) {
 
 int nw_ipc_get_handle(const void *d_ptr, void *handle) {
     if (!d_ptr || !handle) return NW_ERR_ARG;
+    if (link_coarse()) return NW_ERR_UNSUPPORTED;  // (a peer would see stale data)
     hipIpcMemHandle_t h;
     NW_HIP_TRY(hipIpcGetMemHandle(&h, const_cast<void *>(d_ptr)));
     std::memcpy(handle, &h, sizeof h < NW_IPC_HANDLE_BYTES ? sizeof h : NW_IPC_HANDLE_BYTES);

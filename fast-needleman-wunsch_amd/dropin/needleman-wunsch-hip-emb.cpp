@@ -15,7 +15,8 @@ namespace {
 // device context created at plugin load (see needleman-wunsch-hip.cpp)
 struct Warmup {
     Warmup() {
-        if (!std::getenv("NW_COLD_START")) (void)nw_host_warmup(-1);
+        const char *e = std::getenv("NW_WARM_START");
+        if (e != nullptr && e[0] == '1') (void)nw_host_warmup(-1);
     }
 } g_warmup;
 }  // namespace

@@ -451,9 +451,14 @@ def _sweep(args, partition: str, rank: int, world: int, dev: int, scheme, blocks
     waves = args.waves
     if args.share_gpu and waves == 0:
         waves = max(1, resident_waves(dev, sub, nc, kernel) // world)
-    # --debug-withhold-rank r: rank r never publishes its boundary (the fail-fast test)
-    withhold = getattr(args, "debug_withhold_rank", -1) == rank
+    # --debug-withhold-rank r: rank r publishes its boundary into a private buffer of
+    # its own instead of its consumer's (the fail-fast test)
+    withhold = getattr(args, "debug_withhold_rank", -1) == rank and out_bufs is not None
+    if withhold:
+        decoys = [nwhip.Feed(n2, dev) if cols else nwhip.Feed(n1, dev) if hrows else
+                  nwhip.Halo(n1, dev, regions=m) for _ in range(2)]
     warm_tmo = int(getattr(args, "warmup_timeout_ms", 5000))
+    clean = False
     try:
         preflight(rank, world, stream, links_in, out_bufs, link_word, prod_word)
 
@@ -466,7 +471,7 @@ def _sweep(args, partition: str, rank: int, world: int, dev: int, scheme, blocks
                 nwhip.link_wait(link_word.ptr, k - 2, stream, timeout_ms=timeout_ms, ctx=ctx)
             if ev is not None:
                 ev[0].record(stream)
-            hout = out_bufs[b] if out_bufs is not None and not withhold else None
+            hout = (decoys[b].ptr if withhold else out_bufs[b]) if out_bufs is not None else None
             kw = dict(tag=k, scheme=scheme, waves=waves, stream=stream, substrips=sub, strip_waves=nc,
                       kernel=kernel, timeout_ms=timeout_ms)
             if cols:
@@ -514,20 +519,26 @@ def _sweep(args, partition: str, rank: int, world: int, dev: int, scheme, blocks
         last = table[m - 1] if cyc else table
         score = int(last[rows - 1, ncols - 1].item()) if rank == world - 1 else None
         del last
+        clean = True
     finally:
-        torch.cuda.synchronize()
-        dist.barrier()
-        if out_bufs:
-            for x in out_bufs:
-                nwhip.ipc_close_handle(x)
-        if prod_word is not None:
-            nwhip.ipc_close_handle(prod_word)
-        dist.barrier()
-        for x in (links_in or []) + ([link_word] if link_word else []):
-            x.free()
-        ctx.close()
-        del table
-        torch.cuda.empty_cache()
+        # after a failure on any rank, leave at once (no collective: the ranks may
+        # have failed at different points); torch.distributed.run then ends the
+        # others, and the buffers go with the processes
+        if not clean:
+            print(f"rank {rank}: band sweep ({partition}) failed", file=sys.stderr, flush=True)
+    torch.cuda.synchronize()
+    dist.barrier()
+    if out_bufs:
+        for x in out_bufs:
+            nwhip.ipc_close_handle(x)
+    if prod_word is not None:
+        nwhip.ipc_close_handle(prod_word)
+    dist.barrier()
+    for x in (links_in or []) + ([link_word] if link_word else []) + (decoys if withhold else []):
+        x.free()
+    ctx.close()
+    del table
+    torch.cuda.empty_cache()
     return {"wall": wall, "status": status, "link_status": link_status, "failure": failure, "kms": kms,
             "score": score, "n1": n1, "n2": n2, "shape": [sub, nc], "kernel": kernel, "rows": rows,
             "start": start, "blocks": m, "block_rows": h}

@@ -88,10 +88,12 @@ def torch():
 
 
 def granules(torch, values: np.ndarray, tag: int, size: int):
-    """{tag, value} granules (tag in the high word) as an int64 CUDA tensor of `size`."""
+    """{tag, value} granules (tag in the high word) as an int64 CUDA tensor of `size`:
+    the values, then padding granules carrying the tag (a producer publishes whole
+    64-granule blocks; the consumer takes them 16 at a time)."""
     v = values.astype(np.int64) & 0xFFFFFFFF
-    out = np.zeros(size, np.int64)
-    out[:v.size] = (np.int64(tag) << 32) | v
+    out = np.full(size, np.int64(tag) << 32, np.int64)
+    out[:v.size] |= v
     return torch.from_numpy(out).cuda()
 
 
@@ -121,7 +123,8 @@ def test_config4_rank_band_alone(torch, g, rank, sweep):
             hin = granules(torch, halo_row.astype(np.int64) - GAP * (j + start), tag, fsize)
             hout = None if last else torch.zeros(fsize, dtype=torch.int64, device="cuda")
             ctx.fill_tband(d1, d2, tab, row0=start, feed_in=hin, feed_out=hout, tag=tag)
-        assert ctx.status() == nwhip.NW_OK
+        st = ctx.status()
+        assert st == nwhip.NW_OK, f"status {st}, first failure {ctx.debug_failure()}"
         want_last = full_row(g, start + rows - 1)
         np.testing.assert_array_equal(tab[rows - 1, :N + 1].cpu().numpy(), want_last)
         np.testing.assert_array_equal(tab[:rows, N].cpu().numpy(), g["last_col"][start:start + rows])

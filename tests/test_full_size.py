@@ -198,8 +198,9 @@ def test_config4_band_geometry(torch, sweep):
     """BASELINE config 4's row bands (524288 columns, 8 bands, mpi-horz partition) with
     4096 rows per band, concurrently on one device through the in-kernel halo hand-off
     (the 8-GPU run uses the same kernels with the halo in peer HBM), swept in vertical
-    strips (LocalBands) and in horizontal strips (LocalTBands, the bench's main leg):
-    every row of every band against the whole-table golden rows."""
+    strips (LocalBands, the bench's `rows_contiguous` leg) and in horizontal strips
+    (LocalTBands, the `rows_horizontal` leg): every row of every band against the
+    whole-table golden rows."""
     import nw_bands
     n1, n2, P = 524288, 32767, 8
     g = big_rows(n1, n2, (1, 0, -1))
