@@ -45,6 +45,9 @@ __device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
 __device__ __forceinline__ uint64_t gran_load(const uint64_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, NW_GRAN_SCOPE);
 }
+__device__ __forceinline__ uint64_t gran_load(const __attribute__((address_space(1))) uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, NW_GRAN_SCOPE);
+}
 __device__ __forceinline__ void gran_store(uint64_t *p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, NW_GRAN_SCOPE);
 }
@@ -73,6 +76,17 @@ __device__ __forceinline__ void ctr_store(int32_t *p, int32_t v) {
 // the next use of any -- once per iteration, on the fast path too.  A call
 // drains the counters on the slow path only (the callee's entry waits), so the
 // fast path keeps counted vmcnt(N) waits.
+//
+// The polls are PIPELINED: 4 loads of the granules stay in flight, issued
+// kPollGap x 64 cycles apart, and each is checked as it returns (in-order vmcnt)
+// and re-issued at once.  A serial poll sees a granule that became visible at t_v
+// only at t_v + 1.5 load latencies on average (the poll in flight missed it by up
+// to one latency, the next takes another); with polls in flight every ~0.2 us
+// the delay is about half a latency plus the gap -- about 1 us less per hand-off
+// under load (2.5-3 us latency, MI355X_MICROARCH.md handoff-1to1 L->L).  The
+// error word and the watchdog are checked every 32 polls (the error word's load
+// waits for the polls before it).
+#ifdef NW_POLL_SERIAL  // A/B: one poll at a time
 __device__ __noinline__ uint64_t wait_chunk(const uint64_t *g, uint32_t tag, int c,
                                             uint32_t *ctrl, uint32_t site, uint64_t tmo) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -89,6 +103,52 @@ __device__ __noinline__ uint64_t wait_chunk(const uint64_t *g, uint32_t tag, int
         }
     }
 }
+#else
+constexpr int kPollGap = 8;  // s_sleep units (64 cycles): ~0.2 us at 2.4 GHz
+typedef const __attribute__((address_space(1))) uint64_t *gran_gptr;
+__device__ __noinline__ uint64_t wait_chunk(const uint64_t *gp, uint32_t tag, int c,
+                                            uint32_t *ctrl, uint32_t site, uint64_t tmo) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    const int lane = threadIdx.x & 63;
+    const bool in_chunk = (lane >> 4) == c;
+    auto seen = [&](uint64_t v) { return __all(!in_chunk || (uint32_t)(v >> 32) == tag); };
+    // global (not flat) loads: vmcnt only, so each check waits for its own poll
+    const gran_gptr g = (gran_gptr)gp;
+    uint64_t v0 = gran_load(g);
+    __builtin_amdgcn_s_sleep(kPollGap);
+    uint64_t v1 = gran_load(g);
+    __builtin_amdgcn_s_sleep(kPollGap);
+    uint64_t v2 = gran_load(g);
+    __builtin_amdgcn_s_sleep(kPollGap);
+    uint64_t v3 = gran_load(g);
+    uint32_t round = 0;
+    for (;;) {
+        // (the sleep before each re-issue keeps the polls spaced, also after the
+        // error-word check below has drained them)
+        if (seen(v0)) return v0;
+        __builtin_amdgcn_s_sleep(kPollGap);
+        v0 = gran_load(g);
+        if (seen(v1)) return v1;
+        __builtin_amdgcn_s_sleep(kPollGap);
+        v1 = gran_load(g);
+        if (seen(v2)) return v2;
+        __builtin_amdgcn_s_sleep(kPollGap);
+        v2 = gran_load(g);
+        if (seen(v3)) return v3;
+        __builtin_amdgcn_s_sleep(kPollGap);
+        v3 = gran_load(g);
+        // the error word and the watchdog every 8 rounds (32 polls): the error
+        // word's load drains the polls in flight
+        if ((++round & 7u) == 0u) {
+            if (ctrl_load(ctrl + 1) != 0u) return v3;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > tmo) {
+                give_up(ctrl, 1u, site, gp, tag, (int64_t)(v3 >> 32));
+                return v3;
+            }
+        }
+    }
+}
+#endif
 
 // Leading 16-row chunks of a block whose granules all carry `tag` (0 .. 4).
 __device__ __forceinline__ int chunks_ready(uint64_t v, uint32_t tag) {

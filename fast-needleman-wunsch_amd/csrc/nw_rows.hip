@@ -559,6 +559,7 @@ __device__ __forceinline__ void feeder_in(const FillArgs &A, char *__restrict__ 
     const uint64_t tmo = A.timeout_ticks;
     int32_t avail = 0, consv = 0;
     uint64_t t_last = __builtin_amdgcn_s_memrealtime();
+#ifdef NW_POLL_SERIAL  // A/B: one load in flight
     while (avail < nrow_it) {
         // feed-ring space for rows avail .. avail+63
         const int32_t need = avail + kWave - kFeedRows;
@@ -585,6 +586,77 @@ __device__ __forceinline__ void feeder_in(const FillArgs &A, char *__restrict__ 
             __builtin_amdgcn_s_sleep(1);
         }
     }
+#else
+    // Pipelined: 4 loads of 64 granules in flight, each from the first row not yet
+    // delivered when it was issued (its base b); a load that returns delivers the
+    // leading run of matching rows from `avail` (rows b + lane, lanes avail - b ..)
+    // and is re-issued at the new `avail` after kPollGap.  A granule that becomes
+    // visible is then seen about half a load latency + the gap later instead of
+    // ~1.5 latencies (nw_dev.h wait_chunk).  The error word and the watchdog are
+    // checked every 32 loads without progress (the error word's load drains the
+    // loads in flight).
+    typedef const __attribute__((address_space(1))) uint64_t *gptr;
+    const gptr gg = (gptr)gin;
+    int32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0;
+    uint64_t g0 = gran_load(gg + min(lane, nrow_it - 1));
+    uint64_t g1 = g0, g2 = g0, g3 = g0;
+    bool done = false;
+    uint32_t idle = 0;
+    // one pipeline step on slot (g, b): deliver, then re-issue
+    auto step = [&](uint64_t &g, int32_t &b) {
+        const int32_t k = avail - b;  // lanes below k hold rows already delivered
+        const int32_t r = b + lane;
+        const uint64_t ok = __ballot(r < nrow_it && (uint32_t)(g >> 32) == tag_in);
+        const uint64_t run = k < 64 ? ~(ok >> k) : 0ull;
+        const int n = k >= 64 ? 0 : run == 0ull ? 64 - k : min((int)__builtin_ctzll(run), 64 - k);
+        if (n > 0) {
+            const int32_t need = avail + n - kFeedRows;  // feed-ring space for the new rows
+            if (consv < need) {
+                consv = wait_counter(cons, need, A.ctrl, 16, tmo);
+                if (consv == kDead) {
+                    done = true;
+                    return;
+                }
+            }
+            if (lane >= k && lane < k + n) feed[(uint32_t)r & (kFeedRows - 1)] = (int32_t)(uint32_t)g;
+            lds_order();
+            avail += n;
+            ctr_store(avail_w, avail);
+            t_last = __builtin_amdgcn_s_memrealtime();
+            idle = 0;
+        } else {
+            __builtin_amdgcn_s_sleep(kPollGap);
+            if ((++idle & 31u) == 0u) {
+                if (ctrl_load(A.ctrl + 1) != 0u) {
+                    done = true;
+                    return;
+                }
+                if (__builtin_amdgcn_s_memrealtime() - t_last > tmo) {
+                    give_up(A.ctrl, 1u, 13, gin + min(avail, nrow_it - 1), tag_in, (int64_t)(g >> 32));
+                    done = true;
+                    return;
+                }
+            }
+        }
+        b = avail;
+        g = gran_load(gg + min(avail + lane, nrow_it - 1));
+    };
+    __builtin_amdgcn_s_sleep(kPollGap);
+    g1 = gran_load(gg + min(lane, nrow_it - 1));
+    __builtin_amdgcn_s_sleep(kPollGap);
+    g2 = gran_load(gg + min(lane, nrow_it - 1));
+    __builtin_amdgcn_s_sleep(kPollGap);
+    g3 = gran_load(gg + min(lane, nrow_it - 1));
+    while (!done && avail < nrow_it) {
+        step(g0, b0);
+        if (done || avail >= nrow_it) break;
+        step(g1, b1);
+        if (done || avail >= nrow_it) break;
+        step(g2, b2);
+        if (done || avail >= nrow_it) break;
+        step(g3, b3);
+    }
+#endif
     ctr_store(avail_w, kDone);
 }
 
