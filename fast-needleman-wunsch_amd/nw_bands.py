@@ -738,6 +738,26 @@ def run_bands(args) -> dict | None:
 cpu_baseline_fn = None  # bench.py installs its cpu_baseline (rank 0 only reports it)
 
 
+def band_traffic(n1: int, rows: int, sweep: str):
+    """HBM bytes per launch of one GPU's row-band kernel (WRITE_SIZE + 2 x FETCH_SIZE)
+    from the committed rocprofv3 PMC record of that band filled alone on one GPU
+    (profiles/pmc_traffic.json, tools/r04/profile.sh: config 4's last band, 65538 x
+    524289), and where it came from; (None, None) for a geometry without a record."""
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
+                        "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        d = json.load(f)
+    key = f"nw_fill_rowband_{rows}x{n1 + 1}:{sweep}"
+    e = d.get(key)
+    if not e:
+        return None, None
+    return e["hbm_bytes_per_launch"], (f"profiles/pmc_traffic.json [{key}], {e.get('round', '?')} "
+                                       f"{e.get('date', '')}: the band filled alone on one GPU, its kernel's "
+                                       f"WRITE_SIZE + 2 x FETCH_SIZE")
+
+
 def _line(args, world: int, scheme, part: str, ms: list) -> dict:
     """The bench JSON line of one partition from every rank's _sweep result."""
     cols = part == "cols"
@@ -753,6 +773,9 @@ def _line(args, world: int, scheme, part: str, ms: list) -> dict:
     per_gpu_bytes = table_bytes / world
     achieved = per_gpu_bytes / (ms_step * 1e6)  # GB/s per GPU, whole step (incl. pipeline ramp)
     kern = {0: "auto", 1: "strips", 2: "panels"}[m0["kernel"]]
+    # per-GPU HBM traffic of the largest band (the last one) where a PMC record exists
+    traffic, traffic_src = (band_traffic(n1, ml["rows"], "horizontal" if part == "hrows" else "vertical")
+                            if part in ("rows", "hrows") and ml["blocks"] == 1 else (None, None))
     common = {"n1": n1, "n2": n2, "scheme": list(scheme), "bands": world, "table_bytes": int(table_bytes),
               "kernel": kern, "shape": m0["shape"], "control_plane": "torch.distributed gloo (setup, barriers)",
               "launches": "back to back, buffers by launch parity, link-word flow control (nw_link_*)",
@@ -801,7 +824,8 @@ def _line(args, world: int, scheme, part: str, ms: list) -> dict:
         "score_ok": (want == score) if want is not None else None,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                     "traffic": None, "basis": "per GPU: band table bytes / ms_per_step (whole step)",
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "basis": "per GPU: band table bytes / ms_per_step (whole step)",
                      "kernel_ms_avg_per_rank": [round(m["kms"], 3) for m in ms]},
         "cpu_baseline": None,
         "kernel": nwhip.version(),

@@ -17,6 +17,7 @@ ap.add_argument("--flags", type=int, default=0)
 ap.add_argument("--sub", type=int, default=0)
 ap.add_argument("--nc", type=int, default=0)
 ap.add_argument("--save", default="")
+ap.add_argument("--sw", action="store_true", help="Smith-Waterman mode, scheme (1,-1,-1)")
 args = ap.parse_args()
 ctx = nwhip.Context(0)
 n = args.n
@@ -27,9 +28,13 @@ nstrips = (n + 1 + 63) // 64
 tr = torch.zeros(nstrips * 24, dtype=torch.int64, device="cuda")
 for w in [int(x) for x in args.waves.split(",")]:
     ctx.set_trace(None)
-    r0 = ctx.fill(s1, s2, tab, waves=w, flags=args.flags, substrips=args.sub, strip_waves=args.nc)
+    kw = dict(waves=w, flags=args.flags, substrips=args.sub, strip_waves=args.nc)
+    if args.sw:
+        kw.update(mode=nwhip.MODE_SW, kernel=nwhip.KERNEL_STRIPS)
+    sch = (1, -1, -1) if args.sw else (1, 0, -1)
+    r0 = ctx.fill(s1, s2, tab, sch, **kw)
     ctx.set_trace(tr)
-    r = ctx.fill(s1, s2, tab, waves=w, flags=args.flags, substrips=args.sub, strip_waves=args.nc)
+    r = ctx.fill(s1, s2, tab, sch, **kw)
     nstrips = r.strips
     ctx.set_trace(None)
     t = tr[: nstrips * 24].view(nstrips, 24).cpu().numpy().astype(np.float64)
