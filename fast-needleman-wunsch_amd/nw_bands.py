@@ -635,10 +635,10 @@ def legs_for(args) -> list:
     """[(name, partition, blocks per rank)] of a multi-GPU bench: the main one
     first (its value is the line's), then the alternates (--alt-partition).
     Row bands (BASELINE config 4, mpi-horz's contiguous partition) are swept in
-    horizontal strips by default (--band-sweep): band r+1 then starts a strip hop
-    after band r instead of band r's whole height; the
-    vertical sweep of the same bands, the block-cyclic rows and the column bands
-    run as alternates."""
+    vertical strips by default (--band-sweep auto): band r+1's strip k starts when
+    band r's strip k reaches its last row.  The horizontal sweep of the same bands
+    (band r+1 a strip hop behind band r), the block-cyclic rows and the column
+    bands run as alternates."""
     main = getattr(args, "partition", "rows")
     kernel = getattr(args, "kernel", 0)
     m = max(1, getattr(args, "band_blocks", 1))

@@ -36,21 +36,26 @@ g = config4_golden()
 rows, start = nwhip.band_layout(N, P, args.rank)
 k0 = int(np.searchsorted(g["rows"], start))
 k1 = int(np.searchsorted(g["rows"], start + rows - 1))
-assert g["rows"][k0] == start and g["rows"][k1] == start + rows - 1
-halo, want_last = g["full"][k0], g["full"][k1]
+assert g["rows"][k1] == start + rows - 1
+first = start == 0  # band 0: row 0 is the boundary row (no halo)
+assert first or g["rows"][k0] == start
+halo, want_last = (None if first else g["full"][k0]), g["full"][k1]
 ctx = nwhip.Context(0)
 tab = nwhip.Context.alloc_table(N, rows - 1)
 d1 = torch.from_numpy(nwhip.synth(1, N)).cuda()
 d2 = torch.from_numpy(nwhip.synth(2, N)[start:start + rows - 1].copy()).cuda()
 j = np.arange(N + 1, dtype=np.int64)
-vals = halo.astype(np.int64) if args.sweep == "vertical" else halo.astype(np.int64) - GAP * (j + start)
+if not first:
+    vals = halo.astype(np.int64) if args.sweep == "vertical" else halo.astype(np.int64) - GAP * (j + start)
 size = N + 1 if args.sweep == "vertical" else nwhip.feed_bytes(N) // 8
 ts = []
 for rep in range(args.reps + 1):
     tag = 3 + rep
-    gr = np.full(size, np.int64(tag) << 32, np.int64)
-    gr[:N + 1] |= vals & 0xFFFFFFFF
-    hin = torch.from_numpy(gr).cuda()
+    hin = None
+    if not first:
+        gr = np.full(size, np.int64(tag) << 32, np.int64)
+        gr[:N + 1] |= vals & 0xFFFFFFFF
+        hin = torch.from_numpy(gr).cuda()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     if args.sweep == "vertical":
