@@ -460,9 +460,9 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
     // v_perm score tables when every substitution score minus 2*GAP fits int8
     // (the kernel falls back to compares on the device when s1 holds more than
     // kMaxPerm distinct characters).
-    // table bytes are s - 2 GAP in the w form (NW), s (strips) / s - GAP (panels,
-    // the u form) for SW
-    const int32_t off = !sw ? 2 * p->gap : panels ? p->gap : 0;
+    // table bytes are s - 2 GAP in the w form (NW, and SW in the strips), s - GAP
+    // for SW in the panels (the u form)
+    const int32_t off = sw && panels ? p->gap : 2 * p->gap;
     const bool perm_ok = fits_i8(p->match - off) && fits_i8(p->mismatch - off) &&
                          !(p->flags & NW_FLAG_NO_PROFILE);
     if (sw) {

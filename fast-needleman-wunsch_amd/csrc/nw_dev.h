@@ -77,16 +77,15 @@ __device__ __forceinline__ void ctr_store(int32_t *p, int32_t v) {
 // drains the counters on the slow path only (the callee's entry waits), so the
 // fast path keeps counted vmcnt(N) waits.
 //
-// The polls are PIPELINED: 4 loads of the granules stay in flight, issued
-// kPollGap x 64 cycles apart, and each is checked as it returns (in-order vmcnt)
-// and re-issued at once.  A serial poll sees a granule that became visible at t_v
-// only at t_v + 1.5 load latencies on average (the poll in flight missed it by up
-// to one latency, the next takes another); with polls in flight every ~0.2 us
-// the delay is about half a latency plus the gap -- about 1 us less per hand-off
-// under load (2.5-3 us latency, MI355X_MICROARCH.md handoff-1to1 L->L).  The
-// error word and the watchdog are checked every 32 polls (the error word's load
-// waits for the polls before it).
-#ifdef NW_POLL_SERIAL  // A/B: one poll at a time
+// The default poll is SERIAL: one load in flight, s_sleep 1 between polls.
+// NW_POLL_PIPELINED builds the alternative (4 loads in flight, issued kPollGap x
+// 64 cycles apart, each checked as it returns and re-issued): in theory ~1 us less
+// per hand-off (a serial poll sees a granule ~1.5 load latencies after it became
+// visible, a pipelined one ~half a latency + the gap), measured SLOWER on the same
+// box (profiles/r04c_poll_ab.txt): 256k panels 44.9 -> 48.7 ms, SW 64k strip fill
+// 6.3 -> 7.5 ms -- the extra loads of every waiting wave compete with the fill's
+// own traffic.
+#ifndef NW_POLL_PIPELINED
 __device__ __noinline__ uint64_t wait_chunk(const uint64_t *g, uint32_t tag, int c,
                                             uint32_t *ctrl, uint32_t site, uint64_t tmo) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();

@@ -559,7 +559,8 @@ __device__ __forceinline__ void feeder_in(const FillArgs &A, char *__restrict__ 
     const uint64_t tmo = A.timeout_ticks;
     int32_t avail = 0, consv = 0;
     uint64_t t_last = __builtin_amdgcn_s_memrealtime();
-#ifdef NW_POLL_SERIAL  // A/B: one load in flight
+#ifndef NW_POLL_PIPELINED  // default: one load in flight (A/B r04c: pipelined polls
+                            // made the 256k fill 44.9 -> 48.7 ms, nw_dev.h wait_chunk)
     while (avail < nrow_it) {
         // feed-ring space for rows avail .. avail+63
         const int32_t need = avail + kWave - kFeedRows;

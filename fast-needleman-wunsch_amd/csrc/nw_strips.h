@@ -191,10 +191,9 @@ __device__ __forceinline__ void load_packs(const u32x4 *__restrict__ q, int j, i
 // (serial.cpp:23-24); ms' / mm' / the table bytes have 2*GAP pre-subtracted
 // because the cells hold w = t - GAP*(i+j).
 //   SUB_PERM_SW / SUB_GEN_SW : Smith-Waterman (local alignment, BASELINE config 5):
-//              the cells hold t itself (plain form: the 0 floor is not constant
-//              in the w form) and  t = max(0, diag + s, max(up, left) + GAP)
-//              (v_max_i32, v_add, v_max3 after the diag add); the substitution
-//              as SUB_PERM / SUB_GEN without the 2*GAP.
+//              t = max(0, diag + s, up + GAP, left + GAP) in the same w form as
+//              NW, where the 0 floor becomes z = -GAP*(i+j) (run_iter): the
+//              substitution exactly as SUB_PERM / SUB_GEN.
 
 template <int QB, int KB, int MODE>
 __device__ __forceinline__ int32_t diag_plus_sub(uint32_t w, uint32_t apk, int32_t diag,
@@ -230,7 +229,7 @@ __device__ __forceinline__ int32_t diag_plus_sub(uint32_t w, uint32_t apk, int32
 template <int C>
 struct Lanes {
     int32_t u[C];      // w = t - GAP*(i+j) of the lane's current row, column k
-    int32_t g[C];      // Smith-Waterman: sat0(t + GAP) of u[k] (the next row's "up + GAP")
+    int32_t z;         // Smith-Waterman: the 0 floor in the w form, -GAP*(i + j) of column 0
     int32_t dg;        // w_diag of column 0 for the next step (= last step's w_left)
     int32_t rr;        // RAMP: row of this lane at the current step
     uint32_t apk;      // raw column characters of the lane, byte k = column k
@@ -382,9 +381,9 @@ __device__ __forceinline__ void run_iter(char *__restrict__ lds, int it, const u
 #endif
             int32_t diag = S.dg;
             S.dg = left;
-            // Smith-Waterman: the left neighbour's sat0(t + GAP) (one per step, column 0)
-            int32_t lg = 0;
-            if constexpr (is_sw<MODE>()) lg = (int32_t)__builtin_elementwise_sub_sat((uint32_t)left, (uint32_t)-gap);
+            // Smith-Waterman: this step's floor -GAP*(i + j) of column 0 (one add per
+            // step, off the dependency chain)
+            if constexpr (is_sw<MODE>()) S.z -= gap;
             bool act = true;
             if constexpr (RAMP) {
                 S.rr += 1;
@@ -399,13 +398,14 @@ __device__ __forceinline__ void run_iter(char *__restrict__ lds, int it, const u
                 const int32_t d = diag_plus_sub<q, k, MODE>(w, S.apk, diag, msp, mmp);
                 int32_t x;
                 if constexpr (is_sw<MODE>()) {
-                    // t = max(0, t_diag + s, t_up + GAP, t_left + GAP)
-                    //   = max(t_diag + s, sat0(t_up + GAP), sat0(t_left + GAP))   (GAP <= 0)
-                    // the two saturated terms are >= 0 and carry the floor; sat0(t + GAP)
-                    // = usub_sat(t, -GAP) (cells are >= 0) is formed once per cell below
-                    // -- it is both the next row's up and the next column's left:
-                    // v_add (diag + s), v_max3, v_sub_u32 clamp = 3 VALU per cell
-                    x = max(max(d, S.g[k]), lg);
+                    // t = max(0, t_diag + s, t_up + GAP, t_left + GAP): in the w form
+                    // (w = t - GAP*(i+j), as NW) the gap terms vanish and the 0 floor
+                    // becomes z = -GAP*(i+j):  w = max3(max(w_diag + s', z), w_up, w_left).
+                    // max(w_diag + s', z) does not depend on this step's left value, so
+                    // the chain through the row is one v_max3 per cell, as in NW
+                    // (v_add, v_max, v_max3 = 3 VALU per cell)
+                    const int32_t zk = S.z - gap * k;
+                    x = max(max(max(d, zk), S.u[k]), left);
                 } else {
                     // w = max(w_diag + s - 2 GAP, w_up, w_left)  (w = t - GAP*(i+j))
                     x = max(max(d, S.u[k]), left);
@@ -415,10 +415,6 @@ __device__ __forceinline__ void run_iter(char *__restrict__ lds, int it, const u
                 if constexpr (RAMP) x = act ? x : S.u[k];
                 S.u[k] = x;
                 left = x;
-                if constexpr (is_sw<MODE>()) {
-                    lg = (int32_t)__builtin_elementwise_sub_sat((uint32_t)x, (uint32_t)-gap);
-                    S.g[k] = lg;
-                }
                 if constexpr (L::kGrp) {
                     gq[u & 3] = x;
                 } else {
@@ -503,8 +499,9 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
     typedef Lay<C, NC> L;
     constexpr bool SW = is_sw<MODE>();
     const int32_t gap = A.gap;
-    // the w form (NW) subtracts GAP*(i+j) from every cell; SW cells are plain
-    const int32_t gw = SW ? 0 : gap;
+    // the w form subtracts GAP*(i+j) from every cell (both modes); the top boundary
+    // row is t[0][c] = c*GAP for NW, 0 for SW
+    const int32_t gw = gap, gt = SW ? 0 : gap;
     const int32_t msp = A.match - 2 * gw, mmp = A.mismatch - 2 * gw;
     const int64_t c0 = A.col0 + (int64_t)p * (NC * 64 * C) + (int64_t)j * (64 * C);
     const int64_t cl = c0 + (int64_t)C * lane;  // first column of this lane
@@ -519,7 +516,7 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
     int32_t top[C];
     int32_t bnd0 = 0;
 #pragma unroll
-    for (int k = 0; k < C; ++k) top[k] = (int32_t)((cl + k) * (int64_t)gw);  // SW: row 0 is 0
+    for (int k = 0; k < C; ++k) top[k] = (int32_t)((cl + k) * (int64_t)gt);  // SW: row 0 is 0
     if (B.halo_in != nullptr) {
         const uint64_t h0 = __builtin_amdgcn_s_memrealtime();
         for (;;) {
@@ -559,7 +556,6 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
         const uint32_t a = (c >= 1 && c <= A.n1) ? (uint32_t)A.s1[c - 1] : 0u;
         S.apk |= a << (8 * k);
         S.u[k] = top[k] - (int32_t)((cl + k) * (int64_t)gw);  // w[0][c] = t[0][c] - GAP*c
-        S.g[k] = SW ? (int32_t)__builtin_elementwise_sub_sat((uint32_t)S.u[k], (uint32_t)-gap) : 0;
         if constexpr (MODE == SUB_PERM || MODE == SUB_PERM_SW) {
             const uint32_t x = (c >= 1 && c <= A.n1) ? (uint32_t)A.charmap[a] : 0xFFu;
             const uint32_t msb = (uint32_t)msp & 255u;
@@ -572,6 +568,8 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
     }
     S.dg = 0;
     S.rr = -lane - 1;
+    // SW floor of column 0 at the step before the first (row rr = -lane - 1)
+    S.z = -gap * (int32_t)(-lane - 1 + cl);
     S.cb = 0;
     S.rcol = 0;
     if constexpr (L::kGrp) {
@@ -711,7 +709,8 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
                 // w[r][0] = t[r][0] - GAP*r = t[0][0] with col0 = 1, "minus infinity"
                 // when col0 = 0 (the lane holding column 0 then computes
                 // w[r][0] = w[r-1][0], i.e. t[r][0] = t[r-1][0] + GAP)
-                F.ring[((it & 3) << 6) + lane] = A.col0 ? bnd0 : kNeg;
+                // (SW: t[r][0] = 0, w[r][0] = -GAP*r)
+                F.ring[((it & 3) << 6) + lane] = SW && A.col0 ? -gap * (64 * it + lane) : A.col0 ? bnd0 : kNeg;
             }
             if (traced) tsee = __builtin_amdgcn_s_memrealtime();
         } else if (F.src != FEED_LDS) {
@@ -817,8 +816,7 @@ __device__ __forceinline__ void store_strip(const FillArgs &A, char *__restrict_
     const int32_t f0 = q * BATCH;
     // the ring holds w = t - GAP*(r + c) (run_iter): kc[e] = GAP*(r + c) of element
     // e of this lane's piece in its current batch (wrapping int32, like the cells);
-    // Smith-Waterman rings hold t itself (ug = 0)
-    const uint32_t ug = A.sw ? 0u : (uint32_t)A.gap;
+    const uint32_t ug = (uint32_t)A.gap;  // (both modes: the w form)
     uint32_t kc[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) kc[e] = ug * (uint32_t)(f0 + ro) + ug * (uint32_t)(c0 + 4 * cq + e);
@@ -1057,7 +1055,7 @@ __device__ __forceinline__ void store_strip_grp(const FillArgs &A, char *__restr
     const int64_t rowb = timing ? 0 : A.pitch * 4;
     char *scr = (char *)(A.scratch + (int64_t)blockIdx.x * kScratchWords);
     const int32_t f0 = q * BATCH;
-    const uint32_t ug = A.sw ? 0u : (uint32_t)A.gap;  // SW rings hold t itself
+    const uint32_t ug = (uint32_t)A.gap;  // (both modes: the w form)
     // ring byte offset (within the ring) of column a = 32h + 4cq + k of row f0 + ro,
     // and kc = GAP * (row + column) of it (the ring holds w = t - GAP*(i+j))
     // The right half (columns 32..63) of a row completes 32 steps after the left

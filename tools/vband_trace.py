@@ -26,6 +26,7 @@ ap.add_argument("--waves", default="256,192,160,128,96,64")
 ap.add_argument("--sub", type=int, default=0)
 ap.add_argument("--nc", type=int, default=0)
 ap.add_argument("--flags", type=int, default=0)
+ap.add_argument("--save", default="", help="write start/end (us) per strip to <save>_w<waves>.npz")
 args = ap.parse_args()
 ctx = nwhip.Context(0)
 n1, n2 = args.n1, args.n2
@@ -50,6 +51,9 @@ for w in [int(x) for x in args.waves.split(",")]:
     en = (t[:, 1] - t0) / 100.0
     dur = en - st
     first = dur[: min(ns, r.waves)]
+    if args.save:
+        np.savez(f"{args.save}_w{r.waves}.npz", start=st, end=en, kernel_ms=r.kernel_ms, waves=r.waves,
+                 substrips=r.substrips, strip_waves=r.strip_waves, n1=n1, n2=n2)
     print(f"waves={r.waves} C={r.substrips} NC={r.strip_waves} strips={ns} kernel_ms untraced "
           f"{min(r0.kernel_ms, r1.kernel_ms):.3f} traced {r.kernel_ms:.3f} span_us {en.max():.0f}", flush=True)
     print(f"   traversal us: strip0 {dur[0]:.0f}  first pass med {np.median(first):.0f} max {first.max():.0f}  "
