@@ -725,6 +725,13 @@ int nw_fill_tband_async(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t 
     a.tr = 1;
     a.tr_y0 = tb->row0;
     a.tr_pub = (int32_t)(Rs - 1 - 256 * (s.nstrips - 1));  // the last row's column in the last strip
+    {
+        static const int compute_pub = [] {
+            const char *e = std::getenv("NW_TR_PUB_COMPUTE");
+            return e != nullptr && e[0] == '1';
+        }();
+        a.tr_store_pub = compute_pub ? 0 : 1;
+    }
     if (nw::launch_fill(a, 4, 1, (int)s.waves, stream) != hipSuccess) return NW_ERR_HIP;
     if (nw::launch_tband_edges(tb->feed_in, d_t, pitch, n1, R + 1, p->gap, tb->row0, stream) != hipSuccess)
         return NW_ERR_HIP;

@@ -86,6 +86,8 @@ struct FillArgs {
     // out; tr_pub is the strip-local column of that last row in the last strip.
     int32_t tr;
     int32_t tr_pub;
+    int32_t tr_store_pub;  // 1: the last strip's store waves publish the band's last row
+                           // (0: its compute wave, NW_TR_PUB_COMPUTE=1 for A/B)
     int64_t tr_y0;
 };
 bool sw_shape_ok(int substrips, int strip_waves);

@@ -276,6 +276,8 @@ struct Feed {
 
 // Where a compute wave's right column goes.
 struct Out {
+    bool off;            // publish nothing (a horizontal band's last strip: its store
+                         // waves publish the band's last row, store_strip_tr)
     bool lds;            // into the next compute wave's feed ring (else granules)
     int32_t *ring;       // next wave's feed ring
     int32_t *pub;        // my published-rows counter
@@ -318,7 +320,7 @@ __device__ __forceinline__ void run_iter(char *__restrict__ lds, int it, const u
     int32_t gq[4];  // grouped rings: results of the current 4-step group
     // publish chunk c of block b (lanes i < 16 hold rows 64b + 16c + i)
     auto publish = [&](int c) {
-        if (b < 0) return;
+        if (b < 0 || O.off) return;
         if (O.lds) {
             if (lane < 16) O.ring[(64 * b + 16 * c + lane) & (kFeedRows - 1)] = S.rcol;
             lds_order();
@@ -612,6 +614,7 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
     F.tpub = 0;
     F.tmo = A.timeout_ticks;
     Out O;
+    O.off = A.tr != 0 && feeds && A.tr_store_pub != 0 && (A.flags & 1) == 0;
     O.lds = j + 1 < NC;
     O.ring = (int32_t *)(lds + L::kFeed) + (j + 1 < NC ? j + 1 : j) * kFeedRows;
     O.pub = ctr + 1;
@@ -622,7 +625,7 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
     S.pofs = 0;
     S.pbase = 0;
     if constexpr (!L::kGrp && NC == 1) {
-        if (A.tr != 0 && feeds) {
+        if (A.tr != 0 && feeds && !O.off) {
             const int as = A.tr_pub / C, ks = A.tr_pub % C;
             S.psel = true;
             S.pofs = (lane & 15) - 64 + as;
@@ -639,17 +642,29 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
     uint64_t *gscr = (uint64_t *)(A.scratch + (int64_t)blockIdx.x * kScratchWords) + lane;
 
     const u32x4 *pkp = (const u32x4 *)B.rowpack;
-    // Prefetch pipeline: the left neighbour's granules (feed) and the row words
-    // are loaded PD iterations ahead into NB-deep register rings, so no wait for
-    // a load falls inside the steps.  Buffer = iteration mod NB; all loads
-    // unconditional (clamped indices).  NB is even so that the ring half
-    // (iteration parity) is a function of the buffer index.
+    // Prefetch pipeline: the row words are loaded PD iterations ahead, the left
+    // neighbour's granules (feed) GPD iterations ahead, into NB-deep register
+    // rings, so no wait for a load falls inside the steps.  Buffer = iteration
+    // mod NB; all loads unconditional (clamped indices).  NB is even so that the
+    // ring half (iteration parity) is a function of the buffer index.
+    //   The granule distance sets the hand-off's steady state: a consumer whose
+    //   prefetch of block b (issued GPD iterations before b) finds it incomplete
+    //   takes the slow path, so it settles ~64*GPD steps + the publish lag + a load
+    //   latency behind its producer.  GPD = 1: one iteration (64 steps, 2-4 us)
+    //   still covers the load latency, and each of the chain's hops is 128 steps
+    //   shorter than with GPD = 3 (the row words' distance).
     constexpr int NB = 4, PD = NB - 1;
+#ifdef NW_GPD
+    constexpr int GPD = NW_GPD;
+#else
+    constexpr int GPD = 1;
+#endif
+    static_assert(GPD >= 1 && GPD <= PD, "granule prefetch distance");
     uint64_t gb[NB];
     u32x4 pkb[NB][4];
 #pragma unroll
     for (int i = 0; i < PD; ++i) {
-        gb[i] = gran_load(gin + (int64_t)min(i, lastb) * 64);  // block i, for iteration i
+        if (i < GPD) gb[i] = gran_load(gin + (int64_t)min(i, lastb) * 64);  // block i, for iteration i
         load_packs(pkp, i, lane, pkb[i]);
     }
 
@@ -665,6 +680,7 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
     auto iter = [&](int it, auto cons_c, auto ramp_c) {
         constexpr int CONS = decltype(cons_c)::value;  // it % NB
         constexpr int ISS = (CONS + PD) % NB;          // (it + PD) % NB
+        constexpr int GISS = (CONS + GPD) % NB;        // (it + GPD) % NB
         constexpr int HALF = CONS & 1;                 // it % 2
         constexpr bool RAMP = decltype(ramp_c)::value;
         const bool traced = A.trace != nullptr && it == nblocks / 2;
@@ -717,7 +733,7 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
             // past the last block: every lane's row is beyond n2
             F.ring[((it & 3) << 6) + lane] = kNeg;
         }
-        gb[ISS] = gran_load(gin + (int64_t)min(it + PD, lastb) * 64);
+        gb[GISS] = gran_load(gin + (int64_t)min(it + GPD, lastb) * 64);
         load_packs(pkp, it + PD, lane, pkb[ISS]);
         const int b = it - 1;  // block whose right column this iteration publishes
         uint64_t *gp = (b >= 0 && b < nblocks) ? gout + (int64_t)b * 64 + lane : gscr;
@@ -906,7 +922,7 @@ __device__ __forceinline__ void store_strip(const FillArgs &A, char *__restrict_
             for (int g = 0; g < NG; ++g) {
                 const int32_t r = f + g * NR + ro;
                 if (cq == 0 && r < nrows)
-                    *(int32_t *)(rowp + (int64_t)g * NR * rowb + (int64_t)voff - 4) = bnd0 + r * (int32_t)ug;
+                    *(int32_t *)(rowp + (int64_t)g * NR * rowb + (int64_t)voff - 4) = bnd0 + r * (A.sw ? 0 : (int32_t)ug);
             }
         }
         rowp += NS * BATCH * rowb;
@@ -975,6 +991,24 @@ __device__ __forceinline__ void store_strip_tr(const FillArgs &A, char *__restri
         ctr_store(mine, kDone);
         return;
     }
+    // The band's last strip publishes the band's last row (strip-local row tr_pub =
+    // 4 a* + k*: compute lane a*, piece element k*) into the next band's feed, one
+    // {tag, w} granule per column, from HERE rather than from the compute wave: the
+    // feed is fine-grained memory whose system-scope stores complete slowly, and a
+    // compute wave that issued them waits for them at each of its own prefetch
+    // waits (vmcnt counts stores too).  The 8 lanes (g, a* % 8) hold the row's 32
+    // columns of each batch (block a* / 8, element k*).  Store wave 0 also publishes
+    // column 0 (w = t - GAP*y = 0 for the boundary column t[y][0] = y*GAP) and the
+    // padding granules of the last 64-column block (tag only).
+    const bool tpub = A.tr != 0 && A.tr_store_pub != 0 && A.feed_out != nullptr &&
+                      p == A.strip0 + A.nstrips - 1 && !timing;
+    const int pas = A.tr_pub >> 2, pks = A.tr_pub & 3;
+    const bool plane = tpub && l8 == (pas & 7);
+    const uint64_t ptag = (uint64_t)A.feed_tag << 32;
+    if (tpub && q == 0) {
+        const int32_t x = lane == 0 ? 0 : nx - 1 + lane;
+        if (x < 64 * A.nblocks) gran_store(A.feed_out + x, ptag);
+    }
     // rows of this lane: y = c0 + 4 (8 blk + l8) + k; valid while y <= n1 (the band's last row)
     uint32_t rmask = 0;
 #pragma unroll
@@ -1013,6 +1047,17 @@ __device__ __forceinline__ void store_strip_tr(const FillArgs &A, char *__restri
         // the batch is in registers: release its ring rows before the stores
         lds_order();
         ctr_store(mine, f + NS * BATCH);
+        if (plane) {  // the band's last row, columns f + 4g .. +3 (w form, as the ring holds it)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                uint32_t w = 0;
+#pragma unroll
+                for (int blk = 0; blk < NBLK; ++blk)
+                    if (blk == (pas >> 3)) w = pks == 0 ? v[blk][e][0] : pks == 1 ? v[blk][e][1] : pks == 2 ? v[blk][e][2] : v[blk][e][3];
+                const int32_t x = f + 4 * g + e;
+                if (x < nx) gran_store(A.feed_out + x, ptag | w);
+            }
+        }
         const bool xok = f + 4 * g <= A.n2;  // (a piece reaching past column n2 stays in the pitch slack)
         const uint32_t kf = kb + ug * (uint32_t)f;
         int32_t *col = timing ? base : base + f;
@@ -1184,7 +1229,7 @@ __device__ __forceinline__ void store_strip_grp(const FillArgs &A, char *__restr
             for (int g = 0; g < NU; ++g) {
                 const int32_t r = f + g * 8 + ro;
                 if (cq == 0 && r < nrows)
-                    *(int32_t *)(rp + (int64_t)g * 8 * rowb + (int64_t)voff - 4) = bnd0 + r * (int32_t)ug;
+                    *(int32_t *)(rp + (int64_t)g * 8 * rowb + (int64_t)voff - 4) = bnd0 + r * (A.sw ? 0 : (int32_t)ug);
             }
         }
         if (trace) ts += __builtin_amdgcn_s_memtime() - t0;

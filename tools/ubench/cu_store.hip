@@ -66,5 +66,8 @@ int main(int argc, char **argv) {
         run(store_rows<4>, 4, w, 256, "chip");
         run(store_rows<4>, 4, w, 512, "chip");
     }
+    // how many storing CUs saturate HBM (one workgroup per CU while grid <= 256)
+    for (int w : {4, 8})
+        for (int g : {32, 64, 96, 128, 160, 192, 224, 256}) run(store_rows<4>, 4, w, g, "ncu");
     return 0;
 }
