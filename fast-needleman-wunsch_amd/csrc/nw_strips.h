@@ -650,14 +650,18 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
     //   The granule distance sets the hand-off's steady state: a consumer whose
     //   prefetch of block b (issued GPD iterations before b) finds it incomplete
     //   takes the slow path, so it settles ~64*GPD steps + the publish lag + a load
-    //   latency behind its producer.  GPD = 1: one iteration (64 steps, 2-4 us)
-    //   still covers the load latency, and each of the chain's hops is 128 steps
-    //   shorter than with GPD = 3 (the row words' distance).
+    //   latency behind its producer.  But the wait for a granule load issued one
+    //   iteration ago also waits for the compute wave's own granule STORES of the
+    //   iteration before (vmcnt counts both, in order), which complete slowly
+    //   (system scope).  Measured on one box (profiles/r04e_gpd_ab.txt): GPD = 1
+    //   cuts the (4,1) horizontal band's hop 18.2 -> 11.7 us (band 32.7 -> 31.7 ms)
+    //   but slows the (2,2) SW 64k fill 6.2 -> 7.4 ms; so (4,1) -- the horizontal
+    //   strips' shape -- uses 1, the others 3 (the row words' distance).
     constexpr int NB = 4, PD = NB - 1;
 #ifdef NW_GPD
     constexpr int GPD = NW_GPD;
 #else
-    constexpr int GPD = 1;
+    constexpr int GPD = (C == 4 && NC == 1) ? 1 : 3;
 #endif
     static_assert(GPD >= 1 && GPD <= PD, "granule prefetch distance");
     uint64_t gb[NB];
@@ -899,12 +903,19 @@ __device__ __forceinline__ void store_strip(const FillArgs &A, char *__restrict_
         lds_order();
         ctr_store(mine, f + NS * BATCH);
         if (A.sw) {
+            if (want - f == BATCH && cval == 0xFu) {  // interior batch: every cell counts
 #pragma unroll
-            for (int g = 0; g < NG; ++g) {
-                const bool rok = f + g * NR + ro < nrows;
+                for (int g = 0; g < NG; ++g)
 #pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    vmax = max(vmax, (rok && ((cval >> e) & 1u)) ? (int32_t)v[g][e] : 0);
+                    for (int e = 0; e < 4; ++e) vmax = max(vmax, (int32_t)v[g][e]);
+            } else {
+#pragma unroll
+                for (int g = 0; g < NG; ++g) {
+                    const bool rok = f + g * NR + ro < nrows;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        vmax = max(vmax, (rok && ((cval >> e) & 1u)) ? (int32_t)v[g][e] : 0);
+                }
             }
         }
         if (want - f == BATCH) {
@@ -1194,16 +1205,25 @@ __device__ __forceinline__ void store_strip_grp(const FillArgs &A, char *__restr
                 for (int k = 0; k < 4; ++k) v[g][h][k] += kc[h][k] + kf + ug * (uint32_t)(8 * g);
         // row of unit g of half h: f + 8g + ro - 32h
         if (A.sw) {
+            if (f >= kLagH && f + BATCH <= nrows && cval == 0xFFu) {  // interior batch
 #pragma unroll
-            for (int g = 0; g < NU; ++g)
+                for (int g = 0; g < NU; ++g)
 #pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int32_t r = f + g * 8 + ro - kLagH * h;
-                    const bool rok = r >= 0 && r < nrows;
+                    for (int h = 0; h < 2; ++h)
 #pragma unroll
-                    for (int k = 0; k < 4; ++k)
-                        vmax = max(vmax, (rok && ((cval >> (4 * h + k)) & 1u)) ? (int32_t)v[g][h][k] : 0);
-                }
+                        for (int k = 0; k < 4; ++k) vmax = max(vmax, (int32_t)v[g][h][k]);
+            } else {
+#pragma unroll
+                for (int g = 0; g < NU; ++g)
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int32_t r = f + g * 8 + ro - kLagH * h;
+                        const bool rok = r >= 0 && r < nrows;
+#pragma unroll
+                        for (int k = 0; k < 4; ++k)
+                            vmax = max(vmax, (rok && ((cval >> (4 * h + k)) & 1u)) ? (int32_t)v[g][h][k] : 0);
+                    }
+            }
         }
         const uint64_t t0 = trace ? __builtin_amdgcn_s_memtime() : 0;
         char *rp = rowp + (int64_t)(f - f0) * rowb;
@@ -1319,6 +1339,11 @@ __global__ __launch_bounds__((64 * Lay<C, NC>::kWaves)) void nw_fill_strips(Fill
     // scalar branch (a divergent one would run the untaken side's spin-waits
     // with EXEC = 0, where they never see their counter)
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#ifdef NW_COMPUTE_PRIO
+    // compute waves first at a SIMD's issue arbiter (a store wave shares a SIMD with
+    // a compute wave whenever the workgroup has more than 4 waves)
+    if (wave < NC) __builtin_amdgcn_s_setprio(NW_COMPUTE_PRIO);
+#endif
     for (;;) {
         if (threadIdx.x == 0) {
             for (int w = 0; w < L::kStripWord; ++w) ctl[w] = 0;

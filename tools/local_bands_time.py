@@ -18,10 +18,13 @@ ap.add_argument("--n1", type=int, default=524288)
 ap.add_argument("--n2", type=int, default=65536)
 ap.add_argument("--P", type=int, default=2)
 ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--only", choices=["vertical", "horizontal"], default=None)
 args = ap.parse_args()
 s1 = torch.from_numpy(nwhip.synth(1, args.n1)).cuda()
 s2 = torch.from_numpy(nwhip.synth(2, args.n2)).cuda()
 for name, cls in (("vertical", nw_bands.LocalBands), ("horizontal", nw_bands.LocalTBands)):
+    if args.only not in (None, name):
+        continue
     lb = cls(args.n1, args.n2, args.P)
     lb.fill(s1, s2)
     ts = []

@@ -19,11 +19,22 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--n1", type=int, default=524288)
 ap.add_argument("--n2", type=int, default=65536)
 ap.add_argument("--P", type=int, default=2)
+ap.add_argument("--plain-reps", type=int, default=3, help="untraced fills timed first (events and wall)")
 args = ap.parse_args()
 lb = nw_bands.LocalTBands(args.n1, args.n2, args.P)
 s1 = torch.from_numpy(nwhip.synth(1, args.n1)).cuda()
 s2 = torch.from_numpy(nwhip.synth(2, args.n2)).cuda()
 lb.fill(s1, s2)
+import time  # noqa: E402
+for _ in range(args.plain_reps):
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    w0 = time.perf_counter()
+    a.record()
+    lb.fill(s1, s2)
+    b.record()
+    torch.cuda.synchronize()
+    print(f"untraced fill: events {a.elapsed_time(b):.3f} ms, wall {(time.perf_counter() - w0) * 1e3:.3f} ms", flush=True)
 trs = []
 for r, (rows, _) in enumerate(lb.layout):
     ns = -(-rows // 256) + 1
