@@ -8,11 +8,12 @@ table in HBM before the timed region; nothing copied back inside it).
   N = 1 : BASELINE config 3 -- 262144 x 262144 int32 table (275 GB) on one GPU.
   N > 1 : `value` = row bands across ranks (mpi-horz halo contract, BASELINE
           config 4): n1 = 524288 columns and 65536 rows per GPU (weak scaling;
-          N = 8 is 512k x 512k), contiguous as mpi-horz lays them out; the same
-          bands swept in horizontal strips of 256 rows, the rows dealt to the
-          GPUs in 2 blocks each (block-cyclic) and column bands (mpi-vert: 65536
-          columns per GPU x 524288 rows) run after it as `alt_partitions`.  Launches are enqueued back to back (link-word flow
-          control, no host round trip between them);
+          N = 8 is 512k x 512k), contiguous as mpi-horz lays them out, each band
+          swept in horizontal strips of 256 rows; the same bands in the vertical
+          strips of the single-table fill, the rows dealt to the GPUs in 2 blocks
+          each (block-cyclic) and column bands (mpi-vert: 65536 columns per GPU x
+          524288 rows) run after it as `alt_partitions`.  Launches are enqueued
+          back to back (link-word flow control, no host round trip between them);
           fast-needleman-wunsch_amd/nw_bands.py, DESIGN.md "Multi-GPU".
 
 Prints ONE JSON line on rank 0 (see README / DESIGN.md for field meanings).
@@ -62,9 +63,8 @@ def parse():
     ap.add_argument("--band-sweep", choices=["auto", "horizontal", "vertical"], default="auto",
                     help="N>1 contiguous row bands: swept in horizontal strips of 256 rows along the "
                          "columns (band r+1 starts a strip hop after band r) or in the vertical strips of "
-                         "the single-table fill (band r+1 waits for band r's height); auto = vertical "
-                         "(the horizontal sweep runs a band's leftover row as a second pass today, "
-                         "DESIGN.md section 5); "
+                         "the single-table fill (band r+1 waits for band r's strips to reach its last "
+                         "row); auto = horizontal (the shorter chain at N = 8, DESIGN.md section 5); "
                          "the other runs as an alternate leg")
     ap.add_argument("--kernel", type=int, default=0,
                     help="0 auto, 1 anti-diagonal strips, 2 row-scan panels (nw_params.kernel)")

@@ -114,7 +114,10 @@ struct Lay {
 #ifdef NW_SPR
     static constexpr int kSPR = NW_SPR;  // (tuning builds: make variant DEFS=-DNW_SPR=3)
 #else
-    static constexpr int kSPR = C == 4 ? 3 : C == 1 ? 1 : 2;
+#ifndef NW_SPR2
+#define NW_SPR2 2
+#endif
+    static constexpr int kSPR = C == 4 ? 3 : C == 1 ? 1 : NW_SPR2;
 #endif
 #ifdef NW_BATCH
     static constexpr int kBatch = NW_BATCH;

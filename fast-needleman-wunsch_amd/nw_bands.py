@@ -635,10 +635,10 @@ def legs_for(args) -> list:
     """[(name, partition, blocks per rank)] of a multi-GPU bench: the main one
     first (its value is the line's), then the alternates (--alt-partition).
     Row bands (BASELINE config 4, mpi-horz's contiguous partition) are swept in
-    vertical strips by default (--band-sweep auto): band r+1's strip k starts when
-    band r's strip k reaches its last row.  The horizontal sweep of the same bands
-    (band r+1 a strip hop behind band r), the block-cyclic rows and the column
-    bands run as alternates."""
+    horizontal strips by default (--band-sweep auto): band r+1's first strip trails
+    band r's last strip by a strip hop.  The vertical sweep of the same bands (band
+    r+1's strip k starts when band r's strip k reaches its last row), the
+    block-cyclic rows and the column bands run as alternates."""
     main = getattr(args, "partition", "rows")
     kernel = getattr(args, "kernel", 0)
     m = max(1, getattr(args, "band_blocks", 1))
@@ -647,13 +647,16 @@ def legs_for(args) -> list:
     horiz_ok = kernel != nwhip.KERNEL_PANELS  # (horizontal strips: the (4, 1) strip kernel)
     sweep = getattr(args, "band_sweep", "auto")
     if sweep == "auto":
-        # vertical: the mpi-horz partition gives bands after the first one row more
-        # than a multiple of 256 (the halo row; the last band the remainder), and the
-        # horizontal sweep runs that leftover row as a strip of its own -- a second full
-        # pass when the strips already fill the workers (2 bands of 524288 x 32768 on
-        # one GPU: 33.0 ms vertical against 68.6, profiles/r03z_local_h.txt; DESIGN.md
-        # section 5)
-        sweep = "vertical"
+        # horizontal: band r+1's first strip trails band r's last strip by one hop,
+        # so the node's step is one strip sweep + 256 N - 1 hops (DESIGN.md section 5,
+        # measured inputs, profiles/r04f_*: N = 8 modelled at ~53 ms against ~74-80 ms
+        # for the vertical sweep, whose bands wait for the band above's strips to reach
+        # its last row).  At N = 2 both measure alike: 2 bands of 524288 x 32768 on one
+        # GPU 31.4 ms horizontal / 30.7 vertical (one process), 37.8 / 36.8 ms in two
+        # processes sharing it.  (Round 3's horizontal sweep ran the last band's leftover
+        # row as a second full pass and published the band's last row from the compute
+        # wave; the row-scan finisher and the store-wave publish fixed both.)
+        sweep = "horizontal" if horiz_ok else "vertical"
     horiz = horiz_ok and sweep == "horizontal"
     rows_h = ("rows_horizontal", "hrows", 1)
     rows_v = ("rows_contiguous", "rows", 1)

@@ -229,18 +229,20 @@ def test_withheld_producer_fails_fast(torch_gpu, nproc, withhold, extra):
 
 
 @pytest.mark.parametrize("kw,want", [
-    ({}, ["rows_contiguous", "rows_horizontal", "rows_cyclic", "cols"]),
+    ({}, ["rows_horizontal", "rows_contiguous", "rows_cyclic", "cols"]),
     ({"band_sweep": "horizontal"}, ["rows_horizontal", "rows_contiguous", "rows_cyclic", "cols"]),
+    ({"band_sweep": "vertical"}, ["rows_contiguous", "rows_horizontal", "rows_cyclic", "cols"]),
     ({"band_blocks": 4}, ["rows_cyclic", "rows_horizontal", "rows_contiguous", "cols"]),
     ({"kernel": 2}, ["rows_contiguous", "cols"]),
-    ({"partition": "cols"}, ["cols", "rows_contiguous"]),
-    ({"alt_partition": "none"}, ["rows_contiguous"]),
-    ({"band_rows": 704}, ["rows_contiguous", "rows_horizontal", "cols"]),
-    ({"band_rows": 704, "band_sweep": "horizontal"}, ["rows_horizontal", "rows_contiguous", "cols"]),
+    ({"partition": "cols"}, ["cols", "rows_horizontal"]),
+    ({"alt_partition": "none"}, ["rows_horizontal"]),
+    ({"band_rows": 704}, ["rows_horizontal", "rows_contiguous", "cols"]),
+    ({"band_rows": 704, "band_sweep": "vertical"}, ["rows_contiguous", "rows_horizontal", "cols"]),
 ])
 def test_bench_legs(kw, want):
     """bench.py --gpus N: the row-band leg that is `value` (config 4: contiguous mpi-horz bands,
-    vertical strips unless --band-sweep horizontal or --band-blocks m > 1) and the alternates."""
+    horizontal strips unless --band-sweep vertical, the panel kernel or --band-blocks m > 1) and
+    the alternates."""
     import argparse
     a = dict(partition="rows", kernel=0, band_blocks=1, band_sweep="auto", alt_partition=None,
              band_rows=65536)
