@@ -124,7 +124,21 @@ struct Lay {
 #else
     static constexpr int kBatch = C == 4 ? 8 : 16;
 #endif
-    static constexpr int kWaves = NC * (1 + kSPR);
+    // FEEDER wave (opt-in build NW_FEEDER; one per workgroup, the last): polls the
+    // left strip's granules and fills compute wave 0's feed ring + counter (ctl word
+    // kFeedWord), so that wave 0 waits on LDS only.  Measured (profiles/
+    // r04g_feeder_ab.txt): hop 11.7 -> 8.5 us on the horizontal band, but the band
+    // 32.7 -> 42.1 ms and the SW fill 6.6 -> 7.0 ms -- the workgroup's extra wave
+    // changed the compute waves' code (run_iter 102 -> 140 cycles per step for
+    // strip 0), so it stays off.  Not for shapes whose workgroup would then exceed
+    // 8 waves (register budget).
+#ifdef NW_FEEDER
+    static constexpr bool kFeeder = NC * (1 + kSPR) < 8;
+#else
+    static constexpr bool kFeeder = false;
+#endif
+    static constexpr int kFeedWord = kStripWord + 2;
+    static constexpr int kWaves = NC * (1 + kSPR) + (kFeeder ? 1 : 0);
     // compute wave: check ring space every kChk steps, publish progress every kPub
     // (the ring's 64 slots of slack are eaten by these granularities: a batch,
     // the check period plus the staleness of the counter it uses, the publish
@@ -603,9 +617,10 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
     // also strip 0 of a horizontal-strip row band below the first
     const bool fed = p == A.strip0 && A.feed_in != nullptr;
     Feed F;
-    F.src = j > 0 ? FEED_LDS : (p > 0 || fed) ? FEED_GRAN : FEED_BOUNDARY;
+    // (with a feeder wave, wave 0's granules arrive through LDS like the later waves' feeds)
+    F.src = j > 0 ? FEED_LDS : (p > 0 || fed) ? (L::kFeeder ? FEED_LDS : FEED_GRAN) : FEED_BOUNDARY;
     F.ring = (int32_t *)(lds + L::kFeed) + j * kFeedRows;
-    F.pub = (const int32_t *)(lds + L::kCtl) + (j > 0 ? j - 1 : 0) * L::kCtlWords + 1;
+    F.pub = (const int32_t *)(lds + L::kCtl) + (j > 0 ? (j - 1) * L::kCtlWords + 1 : L::kFeeder ? L::kFeedWord : 1);
     const bool feeds = p == A.strip0 + A.nstrips - 1 && A.feed_out != nullptr;
     F.tag = fed ? A.feed_tag : A.tagbase + (uint32_t)B.pq;
     F.gap = gap;
@@ -671,7 +686,7 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
     u32x4 pkb[NB][4];
 #pragma unroll
     for (int i = 0; i < PD; ++i) {
-        if (i < GPD) gb[i] = gran_load(gin + (int64_t)min(i, lastb) * 64);  // block i, for iteration i
+        if (!L::kFeeder && i < GPD) gb[i] = gran_load(gin + (int64_t)min(i, lastb) * 64);  // block i, for iteration i
         load_packs(pkp, i, lane, pkb[i]);
     }
 
@@ -740,7 +755,7 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
             // past the last block: every lane's row is beyond n2
             F.ring[((it & 3) << 6) + lane] = kNeg;
         }
-        gb[GISS] = gran_load(gin + (int64_t)min(it + GPD, lastb) * 64);
+        if constexpr (!L::kFeeder) gb[GISS] = gran_load(gin + (int64_t)min(it + GPD, lastb) * 64);
         load_packs(pkp, it + PD, lane, pkb[ISS]);
         const int b = it - 1;  // block whose right column this iteration publishes
         uint64_t *gp = (b >= 0 && b < nblocks) ? gout + (int64_t)b * 64 + lane : gscr;
@@ -792,6 +807,61 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
             tr[15] = tin;
         }
     }
+}
+
+// Feeder wave of strip B.pk (Lay::kFeeder): the left neighbour's right column
+// arrives as {tag, value} granules in 64-row blocks (its last compute wave, or a
+// feed_in of the band / column band to the left, publishes them); this wave polls
+// them -- one 64-granule load, the leading run of rows carrying the tag goes into
+// compute wave 0's feed ring (row r at r mod kFeedRows) and the rows-available
+// counter ctl[kFeedWord] -- so that wave 0's prefetch pipeline holds no granule
+// loads and its waits are LDS waits.  Ring space: row r overwrites row r - 256,
+// read by wave 0's iteration (r - 256) / 64, so the wave waits for wave 0's
+// iterations-done counter.  Serial polls (nw_dev.h wait_chunk): one load in flight.
+template <int C, int NC>
+__device__ __forceinline__ void feed_strip(const FillArgs &A, char *__restrict__ lds, const Blk &B, int lane) {
+    typedef Lay<C, NC> L;
+    int32_t *ctl = (int32_t *)(lds + L::kCtl);
+    int32_t *avail_w = ctl + L::kFeedWord;
+    const int p = B.pk;
+    const bool fed = p == A.strip0 && A.feed_in != nullptr;
+    if (!(p > 0 || fed)) return;  // wave 0 takes the boundary column
+    const int32_t *done0 = ctl + 2;  // compute wave 0: iterations done
+    int32_t *ring = (int32_t *)(lds + L::kFeed);
+    const uint64_t *gin = fed ? A.feed_in : A.gran + (int64_t)((B.pq + A.M - 1) % A.M) * A.gstride;
+    const uint32_t tag = fed ? A.feed_tag : A.tagbase + (uint32_t)B.pq;
+    const int32_t nrow = 64 * A.nblocks;
+    const uint64_t tmo = A.timeout_ticks;
+    int32_t avail = 0, consv = 0;
+    uint64_t t_last = __builtin_amdgcn_s_memrealtime();
+    while (avail < nrow) {
+        const int32_t need = ((avail + 63) >> 6) - 3;  // iterations wave 0 must have finished
+        if (consv < need) {
+            consv = wait_counter(done0, need, A.ctrl, 21, tmo);
+            if (consv == kDead) break;
+        }
+        const int32_t r = avail + lane;
+        const uint64_t g = gran_load(gin + min(r, nrow - 1));
+        const uint64_t ok = __ballot(r < nrow && (uint32_t)(g >> 32) == tag);
+        const int n = ok == ~0ull ? 64 : (int)__builtin_ctzll(~ok);  // leading run
+        if (n > 0) {
+            if (lane < n) ring[(uint32_t)r & (kFeedRows - 1)] = (int32_t)(uint32_t)g;
+            lds_order();
+            avail += n;
+            ctr_store(avail_w, avail);
+            t_last = __builtin_amdgcn_s_memrealtime();
+        } else {
+            if (ctrl_load(A.ctrl + 1) != 0u) break;
+            // twice the bound: a wait of the strip's own compute waves (its halo) or
+            // of the producer upstream is the root cause and must be the one to report
+            if (__builtin_amdgcn_s_memrealtime() - t_last > 2 * tmo) {
+                give_up(A.ctrl, 1u, 22, gin + min(avail, nrow - 1), tag, (int64_t)(g >> 32));
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    ctr_store(avail_w, kDone);  // (also releases wave 0 when the wait gave up: the error word is set)
 }
 
 // Smith-Waterman: fold a store wave's running maximum into the strip's word
@@ -1350,6 +1420,7 @@ __global__ __launch_bounds__((64 * Lay<C, NC>::kWaves)) void nw_fill_strips(Fill
     for (;;) {
         if (threadIdx.x == 0) {
             for (int w = 0; w < L::kStripWord; ++w) ctl[w] = 0;
+            ctl[L::kFeedWord] = 0;
             ctl[L::kStripWord] = (int32_t)atomicAdd(A.ctrl, 1u);
         }
         __syncthreads();
@@ -1378,6 +1449,8 @@ __global__ __launch_bounds__((64 * Lay<C, NC>::kWaves)) void nw_fill_strips(Fill
             } else {
                 compute_strip<C, NC, SUB_GEN>(A, lds, B, wave, lane);
             }
+        } else if (L::kFeeder && wave == L::kWaves - 1) {
+            feed_strip<C, NC>(A, lds, B, lane);
         } else {
             const int b = wave - NC;
             if constexpr (L::kGrp) {
