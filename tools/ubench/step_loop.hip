@@ -5,11 +5,11 @@
 // exactly the code the fill runs.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../../include \
 //         -I../../fast-needleman-wunsch_amd/csrc step_loop.hip -o step_loop
-#include "../../fast-needleman-wunsch_amd/csrc/nw_fill.hip"
+#include "../../fast-needleman-wunsch_amd/csrc/nw_strips.h"
 
 #include <cstdio>
 
-template <int C, int NC, int PUB, int GRAN = 0>
+template <int C, int NC, int PUB, int GRAN = 0, int MODE = nw::SUB_PERM>
 __global__ __launch_bounds__(64) void step_loop(const uint32_t *pkin, int n, int32_t *out,
                                                 unsigned long long *cyc, uint64_t *gsink) {
     typedef nw::Lay<C, NC> L;
@@ -37,6 +37,10 @@ __global__ __launch_bounds__(64) void step_loop(const uint32_t *pkin, int n, int
     S.rb[0] = (uint32_t)lane * (4u * C);
     S.rb[1] = S.rb[0] + 64u * L::kSlot;
     S.rc[0] = S.rc[1] = (uint32_t)((lane & 15) * L::kSlot);
+    S.z = lane;
+    S.psel = false;
+    S.pofs = 0;
+    S.pbase = 0;
     nw::Feed F;
     F.src = nw::FEED_LDS;
     F.ring = (int32_t *)(lds + L::kFeed);
@@ -52,6 +56,7 @@ __global__ __launch_bounds__(64) void step_loop(const uint32_t *pkin, int n, int
     F.tpub = 0;
     F.tmo = 100000000ull * 20ull;
     nw::Out O;
+    O.off = false;
     O.lds = !GRAN;
     O.ring = (int32_t *)(lds + L::kFeed) + (NC > 1 ? nw::kFeedRows : 0);
     O.pub = ctr + 9;
@@ -62,9 +67,9 @@ __global__ __launch_bounds__(64) void step_loop(const uint32_t *pkin, int n, int
     uint32_t ctrl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
     for (int it = 1; it <= n; it += 2) {
-        nw::run_iter<C, NC, nw::SUB_PERM, false, 1>(lds, it, pk, 2, 1, -1, S, ctr, ctr + 3,
+        nw::run_iter<C, NC, MODE, false, 1>(lds, it, pk, 2, 1, -1, S, ctr, ctr + 3,
                                                     PUB ? it - 1 : -1, gsink + blockIdx.x * 64 + lane, 0, O, ctrl, F, lane);
-        nw::run_iter<C, NC, nw::SUB_PERM, false, 0>(lds, it + 1, pk, 2, 1, -1, S, ctr, ctr + 3,
+        nw::run_iter<C, NC, MODE, false, 0>(lds, it + 1, pk, 2, 1, -1, S, ctr, ctr + 3,
                                                     PUB ? it : -1, gsink + blockIdx.x * 64 + lane, 0, O, ctrl, F, lane);
     }
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -100,6 +105,9 @@ int main() {
         run(step_loop<2, 2, 1, 1>, "C=2 NC=2 granules", grid);
         run(step_loop<1, 4, 1>, "C=1 NC=4 publish", grid);
         run(step_loop<4, 1, 1>, "C=4 NC=1 publish", grid);
+        run(step_loop<2, 2, 1, 1, nw::SUB_PERM_SW>, "SW C=2 NC=2 granules", grid);
+        run(step_loop<2, 2, 1, 0, nw::SUB_PERM_SW>, "SW C=2 NC=2 publish", grid);
+        run(step_loop<4, 1, 1, 1, nw::SUB_PERM_SW>, "SW C=4 NC=1 granules", grid);
     }
     return 0;
 }
