@@ -10,7 +10,9 @@ s1 = synth(seed 1), s2 = synth(seed 2), i.i.d. uniform {1,2,3,4}).
 Rectangular tables (RECT): the multi-GPU bench's weak-scaling legs below N = 8
 (bench.py --gpus 2 / 4: row bands of 65536 rows per GPU over 524288 columns, and
 column bands of 65536 columns per GPU over 524288 rows; N = 8 is the 524288 square
-above), from the oracle, keyed "<n1>x<n2>:<scheme>" (nw_bands._golden).
+above; 524288 x 65536 is the one-GPU rehearsal of the row bands -- 2 local bands, and
+bench.py --share-gpu with 2, 4 or 8 ranks of 65536 / N rows), from the oracle, keyed
+"<n1>x<n2>:<scheme>" (nw_bands._golden).
 Writes tests/golden/synth_scores.json: {"<n>:<match>,<mismatch>,<gap>": score}.
 """
 import json
@@ -25,7 +27,7 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 SCHEMES = {(1, 0, -1): "libref_serial.so", (1, -1, -1): "libref_serial_mm1.so"}
 SIZES = [32768, 65536, 131072, 262144, 524288]
-RECT = [(524288, 131072), (524288, 262144), (131072, 524288), (262144, 524288)]
+RECT = [(524288, 65536), (524288, 131072), (524288, 262144), (131072, 524288), (262144, 524288)]
 
 
 def rect_job(n1, n2, scheme):
