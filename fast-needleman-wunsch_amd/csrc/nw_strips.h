@@ -1153,7 +1153,11 @@ __device__ __forceinline__ void store_strip_tr(const FillArgs &A, char *__restri
 #pragma unroll
                 for (int e = 0; e < 4; ++e) o[e] = v[blk][e][k] + kf + ug * (uint32_t)(32 * blk + e + k);
                 if (xok && ((rmask >> (4 * blk + k)) & 1u))
+#ifdef NW_TR_NT  // A/B: non-temporal table stores in the horizontal strips
+                    __builtin_nontemporal_store(o, (u32x4 *)(col + (int64_t)(32 * blk + k) * rowb));
+#else
                     *(u32x4 *)(col + (int64_t)(32 * blk + k) * rowb) = o;
+#endif
             }
     }
     ctr_store(mine, kDone);
