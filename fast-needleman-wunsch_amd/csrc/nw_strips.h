@@ -668,13 +668,13 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
     //   The granule distance sets the hand-off's steady state: a consumer whose
     //   prefetch of block b (issued GPD iterations before b) finds it incomplete
     //   takes the slow path, so it settles ~64*GPD steps + the publish lag + a load
-    //   latency behind its producer.  But the wait for a granule load issued one
-    //   iteration ago also waits for the compute wave's own granule STORES of the
-    //   iteration before (vmcnt counts both, in order), which complete slowly
-    //   (system scope).  Measured on one box (profiles/r04e_gpd_ab.txt): GPD = 1
-    //   cuts the (4,1) horizontal band's hop 18.2 -> 11.7 us (band 32.7 -> 31.7 ms)
-    //   but slows the (2,2) SW 64k fill 6.2 -> 7.4 ms; so (4,1) -- the horizontal
-    //   strips' shape -- uses 1, the others 3 (the row words' distance).
+    //   latency behind its producer.  But an iteration of a fast shape is shorter
+    //   than a loaded load latency, and the wave then stalls on the load it issued
+    //   one iteration before.  Measured on one box (profiles/r04e_gpd_ab.txt): GPD =
+    //   1 cuts the (4,1) horizontal band's hop 18.2 -> 11.7 us (band 32.7 -> 31.7
+    //   ms) but slows the (2,2) SW 64k fill 6.2 -> 7.4 ms (GPD = 2: no change,
+    //   profiles/r04h_step_loop_gpd2.txt); so (4,1) -- the horizontal strips' shape
+    //   -- uses 1, the others 3 (the row words' distance).
     constexpr int NB = 4, PD = NB - 1;
 #ifdef NW_GPD
     constexpr int GPD = NW_GPD;
