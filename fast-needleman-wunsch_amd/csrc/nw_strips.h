@@ -1404,6 +1404,45 @@ constexpr bool sw_shape(int c, int nc) {
     return (c == 2 && nc == 2) || (c == 1 && nc == 4) || (c == 4 && nc == 1) || (c == 2 && nc == 1);
 }
 
+// Role of each physical wave.  Roles are logical indices: compute waves 0 .. NC-1,
+// store waves NC .. (NC + b serves ring b % NC), the feeder last.  A workgroup of
+// more than 4 waves puts two on some SIMD (one issue port); with NW_ROLE_RR the
+// compute roles go to the waves that are alone on their SIMD under round-robin
+// placement (SIMD = wave mod 4, tools/ubench/wave_simd.hip), the store roles to
+// the waves that share one.  Default: identity.
+struct RoleOrder {
+    int logical[16];
+    constexpr RoleOrder(int W, bool rr) : logical{} {
+        int order[16] = {};
+        int k = 0;
+        for (int w = 0; w < W; ++w)
+            if (!rr || (w + 4 >= W && w - 4 < 0)) order[k++] = w;
+        if (rr)
+            for (int w = 0; w < W; ++w)
+                if (!(w + 4 >= W && w - 4 < 0)) order[k++] = w;
+        for (int l = 0; l < W; ++l) logical[order[l]] = l;
+    }
+};
+#ifdef NW_ROLE_RR
+constexpr bool kRoleRR = true;
+#else
+constexpr bool kRoleRR = false;
+#endif
+template <int C, int NC>
+__device__ __forceinline__ int role_of(int w) {
+    constexpr RoleOrder R(Lay<C, NC>::kWaves, kRoleRR);
+    if constexpr (!kRoleRR) {
+        return w;
+    } else {
+        int l = 0;
+        static_for<0, Lay<C, NC>::kWaves>([&](auto wc) {
+            constexpr int pw = decltype(wc)::value;
+            if (w == pw) l = R.logical[pw];
+        });
+        return l;
+    }
+}
+
 // Persistent grid of workgroups of NC compute waves (0 .. NC-1) and NC*kSPR
 // store waves (wave NC + b serves ring b % NC).
 template <int C, int NC, bool UNIT>
@@ -1415,7 +1454,7 @@ __global__ __launch_bounds__((64 * Lay<C, NC>::kWaves)) void nw_fill_strips(Fill
     // wave-uniform in an SGPR: every role / feed / output decision below is a
     // scalar branch (a divergent one would run the untaken side's spin-waits
     // with EXEC = 0, where they never see their counter)
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wave = role_of<C, NC>(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));  // (logical role)
 #ifdef NW_COMPUTE_PRIO
     // compute waves first at a SIMD's issue arbiter (a store wave shares a SIMD with
     // a compute wave whenever the workgroup has more than 4 waves)
