@@ -34,14 +34,21 @@ args = ap.parse_args()
 z = np.load(args.trace)
 st, en = z["start"], z["end"]
 W, n1, n2 = int(z["waves"]), int(z["n1"]), int(z["n2"])
+# A strip's duration in the band-alone run includes its waits for its left neighbour
+# (all strips of a pass start together there); with the traces that record them
+# (`wait`, vband_trace.py since r04) the model uses the work time dur - wait and lets
+# the end-lag constraint rebuild the chain -- older traces give a pessimistic model.
 dur = en - st
+if "wait" in z.files:
+    dur = np.maximum(dur - z["wait"], 0.0)
 S = dur.size
 lag_s = np.diff(st)
 lag_e = np.diff(en)
 h_s = max(0.0, float(np.percentile(lag_s, 5)))
 h_e = max(0.0, float(np.percentile(lag_e, 5)))
 print(f"trace {args.trace}: {S} strips, {W} workers, band {n2} x {n1}, alone {en.max() / 1e3:.2f} ms; "
-      f"strip duration med {np.median(dur):.0f} us (strip 0 {dur[0]:.0f}); start lag p5 {h_s:.2f} us, "
+      f"strip {'work' if 'wait' in z.files else 'duration'} med {np.median(dur):.0f} us (strip 0 {dur[0]:.0f}); "
+      f"start lag p5 {h_s:.2f} us, "
       f"end lag p5 {h_e:.2f} us")
 n1_cells = 262144.0 * 262144.0
 g1 = n1_cells / (args.n1_ms * 1e-3) / 1e9

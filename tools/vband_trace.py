@@ -52,7 +52,8 @@ for w in [int(x) for x in args.waves.split(",")]:
     dur = en - st
     first = dur[: min(ns, r.waves)]
     if args.save:
-        np.savez(f"{args.save}_w{r.waves}.npz", start=st, end=en, kernel_ms=r.kernel_ms, waves=r.waves,
+        np.savez(f"{args.save}_w{r.waves}.npz", start=st, end=en, wait=t[:, 3] / 100.0, kernel_ms=r.kernel_ms,
+                 waves=r.waves,
                  substrips=r.substrips, strip_waves=r.strip_waves, n1=n1, n2=n2)
     print(f"waves={r.waves} C={r.substrips} NC={r.strip_waves} strips={ns} kernel_ms untraced "
           f"{min(r0.kernel_ms, r1.kernel_ms):.3f} traced {r.kernel_ms:.3f} span_us {en.max():.0f}", flush=True)
