@@ -834,6 +834,7 @@ __device__ __forceinline__ void feed_strip(const FillArgs &A, char *__restrict__
     const uint64_t tmo = A.timeout_ticks;
     int32_t avail = 0, consv = 0;
     uint64_t t_last = __builtin_amdgcn_s_memrealtime();
+    uint32_t idle = 0;
     while (avail < nrow) {
         const int32_t need = ((avail + 63) >> 6) - 3;  // iterations wave 0 must have finished
         if (consv < need) {
@@ -850,13 +851,19 @@ __device__ __forceinline__ void feed_strip(const FillArgs &A, char *__restrict__
             avail += n;
             ctr_store(avail_w, avail);
             t_last = __builtin_amdgcn_s_memrealtime();
+            idle = 0;
         } else {
-            if (ctrl_load(A.ctrl + 1) != 0u) break;
-            // twice the bound: a wait of the strip's own compute waves (its halo) or
-            // of the producer upstream is the root cause and must be the one to report
-            if (__builtin_amdgcn_s_memrealtime() - t_last > 2 * tmo) {
-                give_up(A.ctrl, 1u, 22, gin + min(avail, nrow - 1), tag, (int64_t)(g >> 32));
-                break;
+            // the error word and the watchdog every 32 empty polls only: every idle
+            // feeder of the chip re-reading the one error word after each poll is a
+            // hot line (as a scalar poll of it from every wave is, nw_dev.h)
+            if ((++idle & 31u) == 0u) {
+                if (ctrl_load(A.ctrl + 1) != 0u) break;
+                // twice the bound: a wait of the strip's own compute waves (its halo) or
+                // of the producer upstream is the root cause and must be the one to report
+                if (__builtin_amdgcn_s_memrealtime() - t_last > 2 * tmo) {
+                    give_up(A.ctrl, 1u, 22, gin + min(avail, nrow - 1), tag, (int64_t)(g >> 32));
+                    break;
+                }
             }
             __builtin_amdgcn_s_sleep(1);
         }
