@@ -865,7 +865,11 @@ __device__ __forceinline__ void feed_strip(const FillArgs &A, char *__restrict__
                     break;
                 }
             }
+#ifdef NW_FEED_SLEEP  // A/B: the poll period of an idle feeder
+            __builtin_amdgcn_s_sleep(NW_FEED_SLEEP);
+#else
             __builtin_amdgcn_s_sleep(1);
+#endif
         }
     }
     ctr_store(avail_w, kDone);  // (also releases wave 0 when the wait gave up: the error word is set)
