@@ -835,10 +835,17 @@ __device__ __forceinline__ void feed_strip(const FillArgs &A, char *__restrict__
     int32_t avail = 0, consv = 0;
     uint64_t t_last = __builtin_amdgcn_s_memrealtime();
     uint32_t idle = 0;
+    // debug trace (words 19..23): ring-space wait total, the longest no-data streak,
+    // the row it waited for, when it ended, number of streaks over 100 us
+    const bool traced = A.trace != nullptr;
+    uint64_t t_ring = 0, t_max = 0, t_max_end = 0, n_long = 0;
+    int32_t r_max = 0;
     while (avail < nrow) {
         const int32_t need = ((avail + 63) >> 6) - 3;  // iterations wave 0 must have finished
         if (consv < need) {
+            const uint64_t w0 = traced ? __builtin_amdgcn_s_memrealtime() : 0;
             consv = wait_counter(done0, need, A.ctrl, 21, tmo);
+            if (traced) t_ring += __builtin_amdgcn_s_memrealtime() - w0;
             if (consv == kDead) break;
         }
         const int32_t r = avail + lane;
@@ -850,7 +857,17 @@ __device__ __forceinline__ void feed_strip(const FillArgs &A, char *__restrict__
             lds_order();
             avail += n;
             ctr_store(avail_w, avail);
-            t_last = __builtin_amdgcn_s_memrealtime();
+            const uint64_t now = __builtin_amdgcn_s_memrealtime();
+            if (traced && idle > 0) {
+                const uint64_t streak = now - t_last;
+                if (streak > t_max) {
+                    t_max = streak;
+                    r_max = avail - n;
+                    t_max_end = now;
+                }
+                n_long += streak > 10000u ? 1u : 0u;  // > 100 us
+            }
+            t_last = now;
             idle = 0;
         } else {
             // the error word and the watchdog every 32 empty polls only: every idle
@@ -873,6 +890,14 @@ __device__ __forceinline__ void feed_strip(const FillArgs &A, char *__restrict__
         }
     }
     ctr_store(avail_w, kDone);  // (also releases wave 0 when the wait gave up: the error word is set)
+    if (traced && lane == 0) {
+        uint64_t *tr = A.trace + (int64_t)(B.pq - A.strip0) * kTraceWords;
+        tr[19] = t_ring;
+        tr[20] = t_max;
+        tr[21] = (uint64_t)r_max;
+        tr[22] = t_max_end;
+        tr[23] = n_long;
+    }
 }
 
 // Smith-Waterman: fold a store wave's running maximum into the strip's word

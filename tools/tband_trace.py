@@ -46,5 +46,15 @@ for n2 in [int(x) for x in args.n2.split(",")]:
     print(f"  feed waits / strip: med {np.median(t[:, 2]):.0f} max {t[:, 2].max():.0f}; wait us med "
           f"{np.median(t[:, 3]) / 100:.0f} max {t[:, 3].max() / 100:.0f}; ring-space wait us (last wave) med "
           f"{np.median(t[:, 12]) / 100:.0f}", flush=True)
+    if t[:, 20].any():  # feeder wave builds (NW_FEEDER): its stalls
+        mx = t[:, 20] / 100.0
+        order = np.argsort(-mx)[:6]
+        print(f"  feeder: ring-space wait us/strip med {np.median(t[:, 19]) / 100:.0f} max {t[:, 19].max() / 100:.0f}; "
+              f"longest no-data streak us med {np.median(mx):.1f} max {mx.max():.0f}; streaks > 100 us: "
+              f"{int(t[:, 23].sum())} in {int((t[:, 23] > 0).sum())} strips")
+        for q in order:
+            print(f"   strip {q}: longest streak {mx[q]:.0f} us waiting for row {int(t[q, 21])}, ended at "
+                  f"{(t[q, 22] - t0) / 100.0:.0f} us; strip start {st[q]:.0f} end {en[q]:.0f}; "
+                  f"left strip end {en[q - 1] if q > 0 else 0:.0f}", flush=True)
     del tab
     torch.cuda.empty_cache()
