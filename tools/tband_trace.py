@@ -46,6 +46,10 @@ for n2 in [int(x) for x in args.n2.split(",")]:
     print(f"  feed waits / strip: med {np.median(t[:, 2]):.0f} max {t[:, 2].max():.0f}; wait us med "
           f"{np.median(t[:, 3]) / 100:.0f} max {t[:, 3].max() / 100:.0f}; ring-space wait us (last wave) med "
           f"{np.median(t[:, 12]) / 100:.0f}", flush=True)
+    cyc = t[:, 14] / (args.n1 + 1)
+    clk = (t[:, 7] - t[:, 6]) / np.maximum(t[:, 1] - t[:, 0], 1) * 100e6 / 1e9
+    print(f"  compute wave cycles per step inside run_iter: strip 0 {cyc[0]:.1f} med {np.median(cyc):.1f} "
+          f"p90 {np.percentile(cyc, 90):.1f}; shader clock GHz med {np.median(clk):.3f}")
     if t[:, 20].any():  # feeder wave builds (NW_FEEDER): its stalls
         mx = t[:, 20] / 100.0
         order = np.argsort(-mx)[:6]
