@@ -64,6 +64,23 @@ constexpr int kG = 4;            // rows per group (one v_perm word): ring / fee
 constexpr int kBatch = 8;        // rows per store-wave batch
 constexpr int kEnt = 16;         // rows per rowpack entry (16 row characters)
 constexpr int kPanelWords = 8;   // per-panel control words (reset with the wave counters)
+// trips (64 rows) at the start / end of a panel whose left values are loaded after
+// the group instead of one group ahead (a wave then trails its producer by one group,
+// not two: a shorter panel-to-panel hop where it sets the ramp, r04v)
+#if defined(NW_ROWS_LATEFEED)
+constexpr int kLateHead = 1 << 30, kLateTail = 0;
+#else
+#ifdef NW_ROWS_LATE_HEAD
+constexpr int kLateHead = NW_ROWS_LATE_HEAD;
+#else
+constexpr int kLateHead = 0;
+#endif
+#ifdef NW_ROWS_LATE_TAIL
+constexpr int kLateTail = NW_ROWS_LATE_TAIL;
+#else
+constexpr int kLateTail = 0;
+#endif
+#endif
 
 // Store waves per compute wave.  Under full HBM load one 1 KB store holds its
 // wave for ~330 cycles (tools/ubench/panel_store: 4 waves x 1 KB per CU reach
@@ -460,6 +477,8 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
     if (src != SRC_BOUND) fbv = ctr_load(prod_written);
     const uint64_t tstart = __builtin_amdgcn_s_memrealtime();
     for (int trip = 0; trip < ntrips && !dead; ++trip) {
+        constexpr bool kAnyLate = kLateHead > 0 || kLateTail > 0;
+        const bool late = kAnyLate && (trip < kLateHead || trip >= ntrips - kLateTail);
         static_for<0, 16>([&](auto gc) {
             constexpr int g = decltype(gc)::value;
             const int32_t r0 = 64 * trip + kG * g;
@@ -481,12 +500,10 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
             if constexpr ((g & 3) == 0) wload(r0 / kEnt + kWPD, wd[((g >> 2) + kWPD) & 3]);
             // the next group's left values
             const int32_t rn = r0 + kG;
-#ifndef NW_ROWS_LATEFEED
-            if (rn < nrow_it) {
+            if (!late && rn < nrow_it) {
                 if (src != SRC_BOUND) ring_feed(rn + kG);
                 feed_load(rn, lvn);
             }
-#endif
 #pragma unroll
             for (int u = 0; u < kG; ++u) {
                 if (!(g == 0 && u == 0) || trip != 0) row(word, pks, tks, u, lv[u]);
@@ -507,15 +524,13 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
             }
             lds_order();
             ctr_store(ctr, r0 + kG);  // rows written
-#ifdef NW_ROWS_LATEFEED
-            // the next group's left values once this group is out: a wave then trails
-            // its left neighbour by one group instead of two (the read's LDS latency
-            // is exposed at the next group's first row)
-            if (rn < nrow_it) {
+            // late trips: the next group's left values once this group is out: a wave
+            // then trails its left neighbour by one group instead of two (the read's
+            // LDS latency is exposed at the next group's first row)
+            if (late && rn < nrow_it) {
                 if (src != SRC_BOUND) ring_feed(rn + kG);
                 feed_load(rn, lvn);
             }
-#endif
         });
     }
     // every row is in the ring (or the panel is abandoned): release the store
