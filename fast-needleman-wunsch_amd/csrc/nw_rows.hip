@@ -479,6 +479,13 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
     for (int trip = 0; trip < ntrips && !dead; ++trip) {
         constexpr bool kAnyLate = kLateHead > 0 || kLateTail > 0;
         const bool late = kAnyLate && (trip < kLateHead || trip >= ntrips - kLateTail);
+#ifdef NW_ROWS_MIDFEED
+        // mid feed: the next group's left values after this group's second row (a
+        // wave trails its producer by 6 rows instead of 8; 2 rows hide the read)
+        constexpr bool kMid = true;
+#else
+        constexpr bool kMid = false;
+#endif
         static_for<0, 16>([&](auto gc) {
             constexpr int g = decltype(gc)::value;
             const int32_t r0 = 64 * trip + kG * g;
@@ -500,7 +507,7 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
             if constexpr ((g & 3) == 0) wload(r0 / kEnt + kWPD, wd[((g >> 2) + kWPD) & 3]);
             // the next group's left values
             const int32_t rn = r0 + kG;
-            if (!late && rn < nrow_it) {
+            if (!kMid && !late && rn < nrow_it) {
                 if (src != SRC_BOUND) ring_feed(rn + kG);
                 feed_load(rn, lvn);
             }
@@ -515,11 +522,16 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
                 } else {
                     *(int4 *)dst = make_int4(wv[0], wv[1], wv[2], wv[3]);
                 }
+                if (kMid && u == 0 && src != SRC_BOUND) fbv = ctr_load(prod_written);
                 if (u == 1) {
+                    if (kMid && rn < nrow_it) {
+                        if (src != SRC_BOUND) ring_feed(rn + kG);
+                        feed_load(rn, lvn);
+                    }
                     // counters for the next group's checks, read mid-group so that
                     // their latency hides behind rows 2 and 3
                     ring_poll();
-                    if (src != SRC_BOUND) fbv = ctr_load(prod_written);
+                    if (!kMid && src != SRC_BOUND) fbv = ctr_load(prod_written);
                 }
             }
             lds_order();
