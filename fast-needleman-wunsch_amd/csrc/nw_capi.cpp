@@ -246,7 +246,7 @@ const char *nw_strerror(int status) {
 }
 
 const char *nw_version(void) {
-    static char buf[128];
+    static char buf[256];
     std::snprintf(buf, sizeof buf, "libnwhip gfx950 %s", nw::kernel_variant());
     return buf;
 }

@@ -203,6 +203,6 @@ int lds_bytes(int substrips, int strip_waves) {
     }
 }
 
-const char *kernel_variant() { return "strip-NCx64xC-chained-computewaves+storewaves-diagring128-vperm-gran16-wform"; }
+const char *kernel_variant() { return "strips(NCx64xC, compute+store waves, diag ring 128, vperm, gran16, w form) + panels(row scan 4x256, feeder-in/out waves)"; }
 
 }  // namespace nw
