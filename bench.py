@@ -12,9 +12,11 @@ table in HBM before the timed region; nothing copied back inside it).
           swept in horizontal strips of 256 rows; the same bands in the vertical
           strips of the single-table fill, the rows dealt to the GPUs in 2 blocks
           each (block-cyclic) and column bands (mpi-vert: 65536 columns per GPU x
-          524288 rows) run after it as `alt_partitions`.  Launches are enqueued
-          back to back (link-word flow control, no host round trip between them);
-          fast-needleman-wunsch_amd/nw_bands.py, DESIGN.md "Multi-GPU".
+          524288 rows) run after it as `alt_partitions`.  `value` / `ms_per_step`
+          are the PER-FILL latency the reference measures (mpi-horz-driver.cpp:38-83:
+          earliest rank start -> latest rank end, each timed fill alone); the same
+          fills enqueued back to back give `pipelined_ms_per_fill`, reported beside
+          it; fast-needleman-wunsch_amd/nw_bands.py, DESIGN.md "Multi-GPU".
 
 Prints ONE JSON line on rank 0 (see README / DESIGN.md for field meanings).
 """

@@ -212,6 +212,10 @@ bool valid_params(const nw_params *p) {
         return false;
     if (p->kernel != NW_KERNEL_AUTO && p->kernel != NW_KERNEL_STRIPS && p->kernel != NW_KERNEL_PANELS) return false;
     if (p->timeout_ms < 0) return false;
+    // known flag bits only; the debug probes leave the table unwritten, so only with TIMING_ONLY
+    const int32_t dbg = NW_FLAG_DEBUG_DRAIN | NW_FLAG_DEBUG_NO_STORE;
+    if ((p->flags & ~(NW_FLAG_TIMING_ONLY | NW_FLAG_NO_PROFILE | NW_FLAG_NO_FINISH | dbg)) != 0) return false;
+    if ((p->flags & dbg) != 0 && (p->flags & NW_FLAG_TIMING_ONLY) == 0) return false;
     // keep every intermediate far from int32 overflow (|score| < 2^29)
     const int32_t lim = 1 << 12;
     return std::abs(p->match) < lim && std::abs(p->mismatch) < lim && std::abs(p->gap) < lim;
@@ -366,14 +370,14 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
     const bool sw = p->mode == NW_MODE_SW;
     if (sw && (band || cb)) return NW_ERR_UNSUPPORTED;  // (local alignment: single table, config 5)
     if (band && cb) return NW_ERR_ARG;
-    // The kernel holds w = t - GAP*(i+j) in int32 next to a "minus infinity" of
+    // The kernels hold w = t - GAP*(i+j) in int32 next to a "minus infinity" of
     // -2^29: |w| <= (max|score| + |GAP|) * (i + j) must stay below 2^28, with i the
-    // GLOBAL row (a band's halo row carries the values of row band->row0).
-    // Smith-Waterman cells are plain, in [0, max|score| * (min(n1, n2) + 1)].
-    if (sw) {
-        const long long m = std::max({std::llabs(p->match), std::llabs(p->mismatch), std::llabs(p->gap)});
-        if (m * (long long)(std::min(n1, n2) + 1) >= (1LL << 28)) return NW_ERR_ARG;
-    } else {
+    // GLOBAL row (a band's halo row carries the values of row band->row0).  The same
+    // bound holds for Smith-Waterman: its cells are in the w form too (strips: the
+    // 0 floor becomes z = -GAP*(i+j); panels: u = t - GAP*j), so |w|, |z| and the
+    // store waves' GAP*(i+j) reach (max|score| + |GAP|) * (n1 + n2 + 2) although t
+    // itself stays in [0, max|score| * (min(n1, n2) + 1)].
+    {
         const long long m = std::max({std::llabs(p->match), std::llabs(p->mismatch), std::llabs(p->gap)});
         const long long i_max = (long long)n2 + (band ? (long long)band->row0 : 0);
         if ((m + std::llabs(p->gap)) * (long long)(n1 + i_max + 2) >= (1LL << 28)) return NW_ERR_ARG;
@@ -741,6 +745,11 @@ int nw_fill_tband_async(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t 
         nw::FinishArgs f;
         std::memset(&f, 0, sizeof f);
         f.chunk_cols = nw::finish_chunk_cols(n1, c->cus);
+        // debug (tests): NW_DEBUG_FINISH_WIDE=1 forces the 8192-column chunks (K = 32),
+        // otherwise only chosen above 8 chunks per CU (~4.2M columns on 256 CUs)
+        if (const char *e = std::getenv("NW_DEBUG_FINISH_WIDE")) {
+            if (e[0] == '1') f.chunk_cols = nw::finish_chunk_cols(INT64_MAX / 4, c->cus);
+        }
         f.nchunks = (int32_t)((n1 + f.chunk_cols - 1) / f.chunk_cols);
         const size_t need = (size_t)L * (size_t)f.nchunks * sizeof(uint64_t);
         bool fresh = false;
@@ -896,6 +905,9 @@ int nw_ctx_status(nw_ctx *c, void *stream) {
     const bool failed = (w[1] != 0 && w[13] == 0) || w[8] != 0;
     if (w[8] != 0 || w[12] != 0) {
         for (int k = 0; k < 5; ++k) c->last_failure[k] = w[8 + k];
+        // the last launch (poisoned by the folded failure, or failed on its own) is
+        // not folded into [12] until the next reset: count it here
+        if (w[1] != 0 && w[13] == 0) c->last_failure[4] = w[12] + 1;
     } else if (w[1] != 0 && w[13] == 0) {  // the last launch failed (not folded in yet)
         c->last_failure[0] = w[1];
         c->last_failure[1] = w[2];
@@ -1318,9 +1330,10 @@ int nw_debug_failure(nw_ctx *c, uint32_t *out5) {
     NW_HIP_TRY(hipDeviceSynchronize());
     uint32_t w[nw::kCtrlWords] = {};
     NW_HIP_TRY(hipMemcpy(w, c->ctrl, sizeof w, hipMemcpyDeviceToHost));
-    if (w[8] != 0 || w[12] != 0)
+    if (w[8] != 0 || w[12] != 0) {
         for (int k = 0; k < 5; ++k) out5[k] = w[8 + k];
-    else
+        if (w[1] != 0 && w[13] == 0) out5[4] = w[12] + 1;  // + the last launch (nw_ctx_status)
+    } else
         for (int k = 0; k < 5; ++k) out5[k] = c->last_failure[k];
     return NW_OK;
 }

@@ -33,9 +33,11 @@
 // the band's last row is also published into the next band's feed (w form,
 // one granule per column) when the band has a consumer.
 //
-// Waits are bounded by the launch's watchdog (code 3, site 30) and abandoned at
-// once when the error word is set -- e.g. by the fill before it, in which case
-// nothing is computed or published.
+// Waits are bounded by the launch's watchdog (code 1, a granule wait, site 30) and
+// abandoned at once when the error word is set -- e.g. by the fill before it, in
+// which case nothing is computed or published.  The band's last row is published
+// only if the error word is still clear when its row is done (wave 0 re-reads it),
+// so no feed goes out after another chunk has given up.
 #include <hip/hip_runtime.h>
 
 #include "nw_dev.h"
@@ -80,7 +82,7 @@ __device__ __noinline__ int32_t look_back(const uint64_t *look, int32_t k, uint3
         __builtin_amdgcn_s_sleep(1);
         if (ctrl_load(ctrl + 1) != 0u) return kDead;
         if (__builtin_amdgcn_s_memrealtime() - t0 > tmo) {
-            give_up(ctrl, 3u, 30, look + max(j, 0), tag_agg, (int64_t)j);
+            give_up(ctrl, 1u, 30, look + max(j, 0), tag_agg, (int64_t)j);
             return kDead;
         }
     }
@@ -152,6 +154,11 @@ __global__ __launch_bounds__(kFinThreads) void nw_finish_rows(FinishArgs A) {
                     gran_store(look + chunk, ((uint64_t)tag_agg << 32) | (uint32_t)agg);
                 carry = look_back(look, chunk, tag_agg, tag_inc, A.ctrl, A.timeout_ticks);
             }
+            // the last row of a band with a consumer: publish it only while no chunk
+            // has given up (chunk 0 never looks back, and a look-back can end before
+            // another chunk's watchdog fires)
+            if (A.feed_out != nullptr && r == A.nrows - 1 && carry != kDead && ctrl_load(A.ctrl + 1) != 0u)
+                carry = kDead;
             if (lane == 0) {
                 if (carry != kDead)
                     gran_store(look + chunk, ((uint64_t)tag_inc << 32) | (uint32_t)max(carry, agg));

@@ -3,6 +3,8 @@
 #pragma once
 #include <stdint.h>
 
+#include "nw_hip.h"  // (nw_params flag bits the kernels test)
+
 namespace nw {
 
 constexpr int kWave = 64;          // lanes per wavefront

@@ -762,7 +762,7 @@ __device__ __forceinline__ void store_panel(const FillArgs &A, char *__restrict_
     const uint32_t rl = (uint32_t)(w * L::kRing) + (uint32_t)lane * (4u * C);
     int32_t *mine = ctr + 4 + q;
     constexpr int NS = L::kSPW;
-    if (A.flags & 8) {  // debug: no store waves (compute-pace probe, timing only)
+    if (A.flags & NW_FLAG_DEBUG_NO_STORE) {  // debug: no store waves (compute-pace probe, timing only)
         ctr_store(mine, kDone);
         return;
     }

@@ -971,7 +971,7 @@ __device__ __forceinline__ void store_strip(const FillArgs &A, char *__restrict_
     // `rows` further down the ring (the piece offset a * 4C < kSlot survives the mask)
     auto adv = [&](uint32_t x, uint32_t rows) { return (x + rows * L::kSlot) & kMask; };
     int32_t *mine = ctr + 3 + q;
-    if (A.flags & 8) {  // debug: no store waves at all (compute-pace probe, timing only)
+    if (A.flags & NW_FLAG_DEBUG_NO_STORE) {  // debug: no store waves at all (compute-pace probe, timing only)
         ctr_store(mine, kDone);
         return;
     }
@@ -985,7 +985,7 @@ __device__ __forceinline__ void store_strip(const FillArgs &A, char *__restrict_
             lds_order();  // ring reads after the counter that released them
             if (bcol) bnd0 = *bnd0p;
         }
-        if (A.flags & 4) {  // debug: drain the ring without reading it (compute-pace probe)
+        if (A.flags & NW_FLAG_DEBUG_DRAIN) {  // debug: drain the ring without reading it (compute-pace probe)
             rowp += NS * BATCH * rowb;
             lds_order();
             ctr_store(mine, f + NS * BATCH);
@@ -1107,7 +1107,7 @@ __device__ __forceinline__ void store_strip_tr(const FillArgs &A, char *__restri
     int32_t *mine = ctr + 3 + q;
     const int32_t f0 = 1 + q * BATCH;
     ctr_store(mine, f0);
-    if (A.flags & 8) {  // debug: no store waves (compute-pace probe, timing only)
+    if (A.flags & NW_FLAG_DEBUG_NO_STORE) {  // debug: no store waves (compute-pace probe, timing only)
         ctr_store(mine, kDone);
         return;
     }
@@ -1151,7 +1151,7 @@ __device__ __forceinline__ void store_strip_tr(const FillArgs &A, char *__restri
             avail = (sa == kDone || sa == kDead) ? nx : min(sa - 63, nx);
             lds_order();  // ring reads after the counter that released them
         }
-        if (A.flags & 4) {  // debug: drain the ring without reading it (compute-pace probe)
+        if (A.flags & NW_FLAG_DEBUG_DRAIN) {  // debug: drain the ring without reading it (compute-pace probe)
             lds_order();
             ctr_store(mine, f + NS * BATCH);
             continue;
@@ -1261,7 +1261,7 @@ __device__ __forceinline__ void store_strip_grp(const FillArgs &A, char *__restr
     int32_t bnd0 = 0;
     const int32_t *bnd0p = (const int32_t *)(lds + L::kCtl) + L::kStripWord + 1;
     int32_t *mine = ctr + 3 + q;
-    if (A.flags & 8) {  // debug: no store waves at all (compute-pace probe, timing only)
+    if (A.flags & NW_FLAG_DEBUG_NO_STORE) {  // debug: no store waves at all (compute-pace probe, timing only)
         ctr_store(mine, kDone);
         return;
     }
@@ -1375,7 +1375,7 @@ __device__ __forceinline__ void store_strip_grp(const FillArgs &A, char *__restr
     static_assert(BATCH - 1 + 32 + L::kChk - kR <= 0, "store pipeline lookahead exceeds the ring");
     // batches run to f < nrows + 32: the right halves of the last 32 rows
     const int32_t fend = nrows + kLagH;
-    if (A.flags & 4) {  // debug: drain the ring without reading it
+    if (A.flags & NW_FLAG_DEBUG_DRAIN) {  // debug: drain the ring without reading it
         for (int32_t f = f0; f < fend; f += D) {
             wait_rows(f);
             lds_order();

@@ -373,14 +373,16 @@ def _golden(n1: int, n2: int, scheme):
 
 
 def _sweep(args, partition: str, rank: int, world: int, dev: int, scheme, blocks: int = 1) -> dict:
-    """One multi-rank band sweep: `warmup` + `steps` fills enqueued back to back on
-    this rank's stream, halo / feed buffers alternating by launch parity, the
-    producer's stream waiting on the consumer's "done with launch k" link word
-    (nw_link_*) before it rewrites that launch's buffer -- no host round trip
-    between launches.  partition: "rows" (mpi-horz: contiguous row bands, or
-    block-cyclic ones with args.band_blocks > 1 blocks per rank), "cols" (mpi-vert).
-    Returns this rank's measurements (wall time of the timed launches between a
-    barrier + synchronize on both sides)."""
+    """One multi-rank band sweep: `warmup` fills enqueued back to back, then `steps`
+    timed fills EACH ALONE (barrier + synchronize around each; the per-fill latency
+    of mpi-horz-driver.cpp:38-83, gathered by gather_fill_latencies), then `steps`
+    more back to back (the pipelined throughput, reported separately).  Halo / feed
+    buffers alternate by launch parity, the producer's stream waiting on the
+    consumer's "done with launch k" link word (nw_link_*) before it rewrites that
+    launch's buffer -- no host round trip between back-to-back launches.
+    partition: "rows" (mpi-horz: contiguous row bands, or block-cyclic ones with
+    args.band_blocks > 1 blocks per rank), "hrows" (the same bands in horizontal
+    strips), "cols" (mpi-vert).  Returns this rank's measurements."""
     import torch
     import torch.distributed as dist
 
@@ -501,21 +503,44 @@ def _sweep(args, partition: str, rank: int, world: int, dev: int, scheme, blocks
         torch.cuda.synchronize()
         check_ranks(ctx, link_word, rank, world, f"{partition} warmup ({args.warmup} launches, "
                     f"{warm_tmo} ms bound)")
+        # (1) per-fill latency, the reference's metric (mpi-horz-driver.cpp:38-83: the
+        # earliest rank's start to the last rank's end of ONE fill): each timed fill
+        # alone, every rank between a barrier + synchronize before it and a synchronize
+        # after it, stamped on the host's CLOCK_MONOTONIC (one clock for every process
+        # of the node); fill_latencies() takes min start -> max end over the ranks
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                for _ in range(args.steps)]
+        stamps = []
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i, e in enumerate(evs):
+            dist.barrier()
+            torch.cuda.synchronize()
+            a = time.monotonic_ns()
             launch(args.warmup + 1 + i, e)
-        torch.cuda.synchronize()
+            torch.cuda.synchronize()
+            stamps.append((a, time.monotonic_ns()))
         dist.barrier()
         wall = time.perf_counter() - t0
+        # (2) the same fills back to back (link-word flow control only, no barrier
+        # between them): fill k+1 runs on the upper bands while the lower ones still
+        # finish fill k, so wall / steps is a THROUGHPUT -- per-fill time minus most of
+        # the pipeline ramp -- reported separately as pipelined_ms_per_fill
+        dist.barrier()
+        torch.cuda.synchronize()
+        tp = time.perf_counter()
+        for i in range(args.steps):
+            launch(args.warmup + args.steps + 1 + i)
+        torch.cuda.synchronize()
+        dist.barrier()
+        wall_pipe = time.perf_counter() - tp
         # any launch of the timed sweep that gave up (the record is sticky across launches)
         status = ctx.status()
         link_status = link_word.status() if link_word else 0
         failure = ctx.debug_failure() if status != nwhip.NW_OK else None
         kms = float(np.mean([a.elapsed_time(b) for a, b in evs])) if evs else 0.0
+        fills = gather_fill_latencies(stamps, world)
         last = table[m - 1] if cyc else table
         score = int(last[rows - 1, ncols - 1].item()) if rank == world - 1 else None
         del last
@@ -539,9 +564,37 @@ def _sweep(args, partition: str, rank: int, world: int, dev: int, scheme, blocks
     ctx.close()
     del table
     torch.cuda.empty_cache()
-    return {"wall": wall, "status": status, "link_status": link_status, "failure": failure, "kms": kms,
-            "score": score, "n1": n1, "n2": n2, "shape": [sub, nc], "kernel": kernel, "rows": rows,
+    return {"wall": wall, "wall_pipe": wall_pipe, "fills": fills, "status": status, "link_status": link_status,
+            "failure": failure, "kms": kms, "score": score, "n1": n1, "n2": n2, "shape": [sub, nc], "kernel": kernel, "rows": rows,
             "start": start, "blocks": m, "block_rows": h}
+
+
+def fill_latencies(stamps_per_rank) -> dict:
+    """Per-fill latency as mpi-horz-driver.cpp:38-83 defines it: for each timed fill,
+    the LATEST end over the ranks minus the EARLIEST start over the ranks.
+    stamps_per_rank[r][k] = (start_ns, end_ns) of fill k on rank r (one host clock).
+    Returns {"ms": [per fill], "start_skew_ms": [max - min start per fill]}."""
+    nfill = len(stamps_per_rank[0])
+    if any(len(s) != nfill for s in stamps_per_rank):
+        raise ValueError("every rank must report the same number of fills")
+    ms, skew = [], []
+    for k in range(nfill):
+        starts = [s[k][0] for s in stamps_per_rank]
+        ends = [s[k][1] for s in stamps_per_rank]
+        if any(e < a for a, e in zip(starts, ends)):
+            raise ValueError(f"fill {k}: an end stamp precedes its start")
+        ms.append((max(ends) - min(starts)) / 1e6)
+        skew.append((max(starts) - min(starts)) / 1e6)
+    return {"ms": ms, "start_skew_ms": skew}
+
+
+def gather_fill_latencies(stamps, world: int) -> dict:
+    """All-gather every rank's (start, end) stamps over the control plane and reduce
+    them with fill_latencies (every rank gets the same answer)."""
+    import torch.distributed as dist
+    allst = [None] * world
+    dist.all_gather_object(allst, [(int(a), int(b)) for a, b in stamps])
+    return fill_latencies(allst)
 
 
 PING = 0x5A5A0000  # pre-flight marker (never a launch tag: tags count launches from 1)
@@ -606,7 +659,7 @@ def check_ranks(ctx, link_word, rank: int, world: int, what: str) -> None:
     bad = [m for m in allm if m is not None]
     if bad:
         raise RuntimeError(f"band fill failed during the {what}: " + "; ".join(
-            f"band {m['rank']}: {m['status']}, code {m['code']} (1 granule, 2 halo, 3 LDS counter, 4 link wait) "
+            f"band {m['rank']}: {m['status']}, code {m['code']} (1 granule / finisher look-back, 2 halo, 3 LDS counter, 4 link wait) "
             f"at site {m['site']} wave {m['wave']}, needed {m['need']} saw {m['seen']}, "
             f"{m['failed_launches']} failed launches, link status {m['link_status']}, debug_ctrl {m['debug_ctrl']}"
             for m in bad))
@@ -717,7 +770,8 @@ def run_bands(args) -> dict | None:
     alts = {}
     for name, _, _ in plan_[1:]:
         a = _line(args, world, scheme, *legs[name])
-        alts[name] = {k: a[k] for k in ("value", "ms_per_step", "config", "score", "score_golden", "score_ok",
+        alts[name] = {k: a[k] for k in ("value", "ms_per_step", "per_fill_ms", "pipelined_ms_per_fill",
+                                        "pipelined_value", "config", "score", "score_golden", "score_ok",
                                         "roofline")}
     if alts:
         out["alt_partitions"] = alts
@@ -766,22 +820,29 @@ def _line(args, world: int, scheme, part: str, ms: list) -> dict:
     cols = part == "cols"
     m0, ml = ms[0], ms[-1]
     n1, n2 = m0["n1"], m0["n2"]
-    wall_s = max(m["wall"] for m in ms)  # max over ranks
+    wall_s = max(m["wall"] for m in ms)  # max over ranks (the per-fill region, barriers included)
+    pipe_s = max(m["wall_pipe"] for m in ms)
+    fills = m0["fills"]  # the same on every rank (gather_fill_latencies)
     score = ml["score"]
     want = _golden(n1, n2, scheme)
     cells = n1 * n2
-    ms_step = wall_s / args.steps * 1e3
-    value = cells * args.steps / wall_s / 1e9
+    # `value` / `ms_per_step`: the mean per-fill latency (earliest start -> latest end
+    # over the ranks, each fill alone: mpi-horz-driver.cpp:38-83), NOT the back-to-back
+    # throughput, which hides most of the pipeline ramp (pipelined_ms_per_fill)
+    ms_step = float(np.mean(fills["ms"]))
+    value = cells / (ms_step * 1e-3) / 1e9
+    pipe_ms = pipe_s / args.steps * 1e3
     table_bytes = 4.0 * (n1 + 1) * (n2 + 1)
     per_gpu_bytes = table_bytes / world
-    achieved = per_gpu_bytes / (ms_step * 1e6)  # GB/s per GPU, whole step (incl. pipeline ramp)
+    achieved = per_gpu_bytes / (ms_step * 1e6)  # GB/s per GPU over one whole fill (incl. pipeline ramp)
     kern = {0: "auto", 1: "strips", 2: "panels"}[m0["kernel"]]
     # per-GPU HBM traffic of the largest band (the last one) where a PMC record exists
     traffic, traffic_src = (band_traffic(n1, ml["rows"], "horizontal" if part == "hrows" else "vertical")
                             if part in ("rows", "hrows") and ml["blocks"] == 1 else (None, None))
     common = {"n1": n1, "n2": n2, "scheme": list(scheme), "bands": world, "table_bytes": int(table_bytes),
               "kernel": kern, "shape": m0["shape"], "control_plane": "torch.distributed gloo (setup, barriers)",
-              "launches": "back to back, buffers by launch parity, link-word flow control (nw_link_*)",
+              "launches": "buffers by launch parity, link-word flow control (nw_link_*); timed fills one at a time, "
+                           "then back to back for pipelined_ms_per_fill",
               "shared_gpu": bool(args.share_gpu)}
     if cols:
         cfg = {"workload": f"nw_fill_colbands_{n2}x{n1}", "col_width": args.col_width,
@@ -816,6 +877,17 @@ def _line(args, world: int, scheme, part: str, ms: list) -> dict:
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_step, 3),
+        "timing": "per fill: each timed fill alone (barrier + synchronize around it), earliest rank start -> "
+                  "latest rank end on the host's CLOCK_MONOTONIC (mpi-horz-driver.cpp:38-83); value = cells / "
+                  "mean per-fill time",
+        "per_fill_ms": [round(x, 3) for x in fills["ms"]],
+        "start_skew_ms_max": round(max(fills["start_skew_ms"]), 3),
+        "timed_region_ms_per_step": round(wall_s / args.steps * 1e3, 3),
+        "pipelined_ms_per_fill": round(pipe_ms, 3),
+        "pipelined_value": round(cells / (pipe_ms * 1e-3) / 1e9, 2),
+        "pipelined_note": "the same fills enqueued back to back (link-word flow control only): the upper bands "
+                          "start fill k+1 while the lower ones finish fill k, so this is a throughput that hides "
+                          "most of the pipeline ramp -- not the reference's metric",
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -828,7 +900,7 @@ def _line(args, world: int, scheme, part: str, ms: list) -> dict:
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                      "traffic": traffic, "traffic_source": traffic_src,
-                     "basis": "per GPU: band table bytes / ms_per_step (whole step)",
+                     "basis": "per GPU: band table bytes / ms_per_step (one whole fill, pipeline ramp included)",
                      "kernel_ms_avg_per_rank": [round(m["kms"], 3) for m in ms]},
         "cpu_baseline": None,
         "kernel": nwhip.version(),

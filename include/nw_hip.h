@@ -51,9 +51,13 @@ enum {
     NW_FLAG_TIMING_ONLY = 1, /* table stores go to a scratch tile (kernel timing only) */
     NW_FLAG_NO_PROFILE = 2,  /* substitution by byte compares instead of the per-lane
                                 v_perm score tables */
-    NW_FLAG_NO_FINISH = 4    /* nw_fill_tband_async: sweep every row in strips, also a
+    NW_FLAG_NO_FINISH = 4,   /* nw_fill_tband_async: sweep every row in strips, also a
                                 last strip that runs alone as one more pass (default:
                                 such rows go to the row-scan finisher) */
+    /* debug probes of the compute pace: only together with NW_FLAG_TIMING_ONLY
+       (refused otherwise -- the table is not written) */
+    NW_FLAG_DEBUG_DRAIN = 0x100,    /* store waves drain the LDS ring without reading it */
+    NW_FLAG_DEBUG_NO_STORE = 0x200  /* no store waves at all */
 };
 
 /* nw_params.kernel: which gfx950 kernel family fills the table.  Both compute
@@ -444,13 +448,13 @@ int nw_ctx_status(nw_ctx *ctx, void *stream);
 
 /* Debug hooks (diagnosis, not needed for fills).
  * nw_debug_ctrl: the 8 control words of the context's last launch: [0] strip
- *   ticket, [1] error code (0 ok; 1 hand-off granule wait, 2 halo wait, 3 LDS
- *   counter wait expired), [2] site << 24 | wave << 16 | address bits, [3] the
+ *   ticket, [1] error code (0 ok; 1 hand-off granule wait -- strips, panels, the
+ *   finisher's look-back (site 30) --, 2 halo wait, 3 LDS counter wait expired), [2] site << 24 | wave << 16 | address bits, [3] the
  *   value the wait needed, [4] the value it last saw.  Syncs the device.  (A
  *   launch that a recorded failure made give up carries that failure's words.)
  * nw_debug_failure: the first failure recorded on ctx -- code (1 granule wait,
  *   2 halo wait, 3 LDS counter, 4 link wait), site word, need, seen, and the
- *   number of failed launches -- pending, or as the last nw_ctx_status cleared it.
+ *   number of failed launches (the failing one and every launch it poisoned) -- pending, or as the last nw_ctx_status cleared it.
  * nw_debug_set_trace: per-strip timeline buffer (device memory of at least
  *   strips * nw_debug_trace_words() uint64), NULL = off. */
 int nw_debug_ctrl(nw_ctx *ctx, uint32_t *out8);

@@ -93,6 +93,57 @@ def test_gloo_bands_reassemble_the_table(tmp_path, world):
     assert np.load(tmp_path / f"band{world - 1}.npy")[-1, -1] == full[-1, -1]
 
 
+# Synthetic per-rank (start, end) stamps of 3 fills, in ns: rank r starts late by
+# 100 r us, the last rank ends last; fill 2 has a rank that ends first but started
+# earliest -- the latency is still max end - min start over the ranks
+_STAMPS = {
+    0: [(1_000_000, 51_000_000), (100_000_000, 140_000_000), (200_000_000, 230_000_000)],
+    1: [(1_100_000, 52_500_000), (100_200_000, 141_000_000), (199_000_000, 228_000_000)],
+    2: [(1_200_000, 53_000_000), (100_100_000, 150_500_000), (200_300_000, 261_000_000)],
+}
+
+
+def _expected(world):
+    st = [_STAMPS[r] for r in range(world)]
+    return [(max(s[k][1] for s in st) - min(s[k][0] for s in st)) / 1e6 for k in range(3)]
+
+
+def test_fill_latencies_min_start_max_end():
+    """The per-fill latency of mpi-horz-driver.cpp:38-83: earliest start -> latest end."""
+    got = nw_bands.fill_latencies([_STAMPS[r] for r in range(3)])
+    assert got["ms"] == pytest.approx([52.0, 50.5, 62.0])
+    assert got["start_skew_ms"] == pytest.approx([0.2, 0.2, 1.3])
+    with pytest.raises(ValueError):
+        nw_bands.fill_latencies([_STAMPS[0], _STAMPS[1][:2]])
+    with pytest.raises(ValueError):
+        nw_bands.fill_latencies([[(5, 4)]])
+
+
+def _gather_main(rank, world, port, outdir):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
+    got = nw_bands.gather_fill_latencies(_STAMPS[rank], world)
+    with open(os.path.join(outdir, f"fills{rank}.json"), "w") as f:
+        json.dump(got, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.timeout(240)
+def test_gloo_gather_fill_latencies(tmp_path, world):
+    """The cross-rank gather of the bench's N>1 timing over a real gloo world: every
+    rank gets the same per-fill latencies, min start -> max end over ALL ranks."""
+    import torch.multiprocessing as mp
+    mp.spawn(_gather_main, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    want = _expected(world)
+    for r in range(world):
+        got = json.load(open(tmp_path / f"fills{r}.json"))
+        assert got["ms"] == pytest.approx(want)
+
+
 # ------------------------------------------------------------------ GPU
 @pytest.fixture(scope="module")
 def torch_gpu():
@@ -191,6 +242,11 @@ def test_two_process_bands_shared_gpu(torch_gpu, kernel, blocks, sweep):
     want = oracle.score(nwhip.synth(1, n1), nwhip.synth(2, n2))
     assert res["score"] == want and res["n_gpus"] == 2 and res["config"]["n2"] == n2
     alts = res["alt_partitions"]
+    # the per-fill latency is `value` (mpi-horz-driver.cpp:38-83); the back-to-back
+    # throughput is reported beside it, in every leg
+    for leg in [res] + list(alts.values()):
+        assert len(leg["per_fill_ms"]) == 3 and leg["pipelined_ms_per_fill"] > 0
+        assert leg["ms_per_step"] == pytest.approx(float(np.mean(leg["per_fill_ms"])), abs=2e-3)
     assert res["config"].get("blocks_per_gpu", 1) == blocks
     if blocks > 1 or (sweep == "horizontal" and kernel == 1):
         assert alts["rows_contiguous"]["score"] == want and res["rows_legs_agree"]

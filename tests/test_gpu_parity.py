@@ -189,6 +189,17 @@ def test_score_range_refused():
     assert nwhip.score(small, small, (4095, -4095, -4095)) == oracle.score(small, small, (4095, -4095, -4095))
 
 
+@pytest.mark.parametrize("flags", [nwhip.FLAG_DEBUG_NO_STORE, nwhip.FLAG_DEBUG_DRAIN, 1 << 20, 8])
+def test_unknown_or_debug_flags_refused(flags):
+    """Flag bits are checked: unknown bits, and the compute-pace probes (which leave
+    the table unwritten) without NW_FLAG_TIMING_ONLY, are refused (NW_ERR_ARG).
+    (Round 4 shared bits 4 / 8 between NW_FLAG_NO_FINISH and the probes.)"""
+    s = nwhip.synth(1, 300)
+    with pytest.raises(nwhip.NwError) as e:
+        nwhip.fill(s, s, (1, 0, -1), flags=flags)
+    assert e.value.status == nwhip.NW_ERR_ARG
+
+
 def test_band_score_range_refused(torch, ctx):
     """A band's halo row carries global values: the range check uses the band's global
     row (nw_band.row0), so a band of a table the whole-table path refuses is refused too."""
@@ -270,11 +281,12 @@ def test_failure_is_sticky_across_launches(torch, kernel):
         # both the compute waves (code 2, site 4) and the feeder-in wave (granule
         # wait, code 1, site 13) wait on the halo -- whichever expires first records
         wants = [(2, 4)] if kernel == nwhip.KERNEL_STRIPS else [(2, 4), (1, 13)]
-        assert (code, site >> 24) in wants and nfail >= 2
+        assert (code, site >> 24) in wants and nfail == 3  # launch 1 + the two poisoned ones
         if (code, site >> 24) == (2, 4):
             assert need == 7
         assert c.status() == nwhip.NW_ERR_TIMEOUT
         assert c.debug_failure()[0] == code  # as the status read cleared it
+        assert c.debug_failure()[4] == 3
         assert c.status() == nwhip.NW_OK  # cleared
         tab2, r = device_fill(torch, c, s1, s2, (1, 0, -1), kernel=kernel)
         assert r.status == 0

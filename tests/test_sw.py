@@ -184,6 +184,20 @@ def test_config5_sw_64k_vs_golden(torch, scheme):
 
 
 @pytest.mark.gpu
+def test_sw_range_refused(torch, ctx):
+    """Smith-Waterman cells live in the w form too (w = t - GAP*(i+j), the
+    floor z = -GAP*(i+j)), so the NW bound (max|score| + |GAP|) * (n1 + n2 + 2) < 2^28
+    applies: a long, thin table with a large gap is refused, not wrapped."""
+    s1, s2 = nwhip.synth(1, 600000), nwhip.synth(2, 1000)
+    with pytest.raises(nwhip.NwError) as e:
+        nwhip.sw_align(s1, s2, (1, -1, -4000))
+    assert e.value.status == nwhip.NW_ERR_ARG
+    # the same shape with the unit scheme is inside the bound and exact
+    al, ops = nwhip.sw_align(s1[:20000], s2[:300], (1, -1, -1))
+    assert (al.score, al.end_i, al.end_j) == oracle.sw_best(s1[:20000], s2[:300], (1, -1, -1))
+
+
+@pytest.mark.gpu
 def test_sw_refusals(torch, ctx):
     """SW with a positive gap, or on a row band, is refused rather than mis-computed."""
     s = nwhip.synth(1, 100)

@@ -192,6 +192,7 @@ def _tband_chain(torch, s1, s2, P, scheme, waves, flags=0, row_split=None):
         for r in range(P):
             rows, start = oracle.band_layout(n2, P, r) if row_split is None else row_split[r]
             tab = nwhip.Context.alloc_table(n1, rows - 1)
+            tab.fill_(-0x5A5A5A5)  # (torch.empty may hand back an earlier table's memory)
             d2 = torch.from_numpy(s2[start:start + rows - 1].copy()).cuda()
             ctx.fill_tband(d1, d2, tab, row0=start, feed_in=feeds[r - 1] if r > 0 else None,
                            feed_out=feeds[r] if r + 1 < P else None, tag=5, scheme=scheme, waves=waves,
@@ -230,6 +231,31 @@ def test_tband_finisher_rows(torch_gpu, n1, waves, extra):
         gap = scheme[2]
         vals = (pub[0] & 0xFFFFFFFF).astype(np.uint32).view(np.int32).astype(np.int64)
         np.testing.assert_array_equal(vals + gap * (np.arange(n1 + 1) + R), full[R], err_msg=f"feed {scheme}")
+        assert np.all((pub[0] >> 32) == 5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n1", [100, 8191, 8192, 8193, 20000])
+def test_tband_finisher_wide_chunks(torch_gpu, n1, monkeypatch):
+    """the finisher's K = 32 instantiation (8192-column chunks, its own
+    vector-store and tail code) is chosen only above ~4.2M columns; forced here with
+    NW_DEBUG_FINISH_WIDE=1 on small widths (one and several chunks, ragged tails) and
+    checked bit-exactly, with the feed it publishes."""
+    monkeypatch.setenv("NW_DEBUG_FINISH_WIDE", "1")
+    torch = torch_gpu
+    waves, extra = 2, 37
+    R = 256 * waves + extra
+    rng = np.random.default_rng(n1 + 5)
+    s1 = rng.integers(1, 5, n1).astype(np.int8)
+    s2 = rng.integers(1, 5, 2 * R + 1).astype(np.int8)
+    for scheme in [(1, 0, -1), (2, -1, -2)]:
+        full = oracle.fill(s1, s2, scheme)
+        split = [(R + 1, 0), (R + 1, R)]
+        tabs, pub = _tband_chain(torch, s1, s2, 2, scheme, waves, row_split=split)
+        for r, (rows, start) in enumerate(split):
+            np.testing.assert_array_equal(tabs[r], full[start:start + rows], err_msg=f"band {r} {scheme}")
+        vals = (pub[0] & 0xFFFFFFFF).astype(np.uint32).view(np.int32).astype(np.int64)
+        np.testing.assert_array_equal(vals + scheme[2] * (np.arange(n1 + 1) + R), full[R])
         assert np.all((pub[0] >> 32) == 5)
 
 

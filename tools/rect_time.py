@@ -17,7 +17,7 @@ ap.add_argument("--n2", type=int, default=65536)
 ap.add_argument("--shapes", default="4:1,2:2,1:4,2:1")
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--kernel", type=int, default=0, help="0 auto, 1 strips, 2 panels")
-ap.add_argument("--flags", type=int, default=0, help="debug flags (8: no store waves, compute pace)")
+ap.add_argument("--flags", type=int, default=0, help="nw_params.flags (513 = 0x201: timing only + no store waves, the compute pace)")
 args = ap.parse_args()
 ctx = nwhip.Context(0)
 s1 = torch.from_numpy(nwhip.synth(1, args.n1)).cuda()

@@ -17,7 +17,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--n1", type=int, default=524288)
 ap.add_argument("--n2", type=int, default=65536)
 ap.add_argument("--reps", type=int, default=3)
-ap.add_argument("--flags", type=int, default=0, help="debug flags (8: no store waves, compute pace)")
+ap.add_argument("--flags", type=int, default=0, help="nw_params.flags (513 = 0x201: timing only + no store waves, the compute pace)")
 ap.add_argument("--vertical", default="4:1,2:2", help="vertical-strip shapes to time beside it ('' = none)")
 args = ap.parse_args()
 ctx = nwhip.Context(0)
