@@ -36,12 +36,9 @@ __device__ __forceinline__ void give_up(uint32_t *ctrl, uint32_t code, uint32_t 
 // compiler from moving plain loads/stores across the relaxed counter accesses.
 __device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
 // Granules are system-scope: the same loads and stores serve a column band's
-// feed, which lives in the neighbouring GPU's HBM (written over xGMI).
-#ifdef NW_EXP_GRAN_AGENT  // timing experiment: agent-scope granules (no peer feeds)
-#define NW_GRAN_SCOPE __HIP_MEMORY_SCOPE_AGENT
-#else
+// feed, which lives in the neighbouring GPU's HBM (written over xGMI).  (Agent
+// scope on a single GPU measured no faster, profiles/r04u_gran_agent_ab.txt.)
 #define NW_GRAN_SCOPE __HIP_MEMORY_SCOPE_SYSTEM
-#endif
 __device__ __forceinline__ uint64_t gran_load(const uint64_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, NW_GRAN_SCOPE);
 }
@@ -77,15 +74,11 @@ __device__ __forceinline__ void ctr_store(int32_t *p, int32_t v) {
 // drains the counters on the slow path only (the callee's entry waits), so the
 // fast path keeps counted vmcnt(N) waits.
 //
-// The default poll is SERIAL: one load in flight, s_sleep 1 between polls.
-// NW_POLL_PIPELINED builds the alternative (4 loads in flight, issued kPollGap x
-// 64 cycles apart, each checked as it returns and re-issued): in theory ~1 us less
-// per hand-off (a serial poll sees a granule ~1.5 load latencies after it became
-// visible, a pipelined one ~half a latency + the gap), measured SLOWER on the same
-// box (profiles/r04c_poll_ab.txt): 256k panels 44.9 -> 48.7 ms, SW 64k strip fill
-// 6.3 -> 7.5 ms -- the extra loads of every waiting wave compete with the fill's
-// own traffic.
-#ifndef NW_POLL_PIPELINED
+// The poll is SERIAL: one load in flight, s_sleep 1 between polls.  (Round 4
+// measured a pipelined poll -- 4 loads in flight per waiting wave -- SLOWER on the
+// same box, profiles/r04c_poll_ab.txt: 256k panels 44.9 -> 48.7 ms, SW 64k strip
+// fill 6.3 -> 7.5 ms: the extra loads of every waiting wave compete with the
+// fill's own traffic.)
 __device__ __noinline__ uint64_t wait_chunk(const uint64_t *g, uint32_t tag, int c,
                                             uint32_t *ctrl, uint32_t site, uint64_t tmo) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -102,52 +95,6 @@ __device__ __noinline__ uint64_t wait_chunk(const uint64_t *g, uint32_t tag, int
         }
     }
 }
-#else
-constexpr int kPollGap = 8;  // s_sleep units (64 cycles): ~0.2 us at 2.4 GHz
-typedef const __attribute__((address_space(1))) uint64_t *gran_gptr;
-__device__ __noinline__ uint64_t wait_chunk(const uint64_t *gp, uint32_t tag, int c,
-                                            uint32_t *ctrl, uint32_t site, uint64_t tmo) {
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    const int lane = threadIdx.x & 63;
-    const bool in_chunk = (lane >> 4) == c;
-    auto seen = [&](uint64_t v) { return __all(!in_chunk || (uint32_t)(v >> 32) == tag); };
-    // global (not flat) loads: vmcnt only, so each check waits for its own poll
-    const gran_gptr g = (gran_gptr)gp;
-    uint64_t v0 = gran_load(g);
-    __builtin_amdgcn_s_sleep(kPollGap);
-    uint64_t v1 = gran_load(g);
-    __builtin_amdgcn_s_sleep(kPollGap);
-    uint64_t v2 = gran_load(g);
-    __builtin_amdgcn_s_sleep(kPollGap);
-    uint64_t v3 = gran_load(g);
-    uint32_t round = 0;
-    for (;;) {
-        // (the sleep before each re-issue keeps the polls spaced, also after the
-        // error-word check below has drained them)
-        if (seen(v0)) return v0;
-        __builtin_amdgcn_s_sleep(kPollGap);
-        v0 = gran_load(g);
-        if (seen(v1)) return v1;
-        __builtin_amdgcn_s_sleep(kPollGap);
-        v1 = gran_load(g);
-        if (seen(v2)) return v2;
-        __builtin_amdgcn_s_sleep(kPollGap);
-        v2 = gran_load(g);
-        if (seen(v3)) return v3;
-        __builtin_amdgcn_s_sleep(kPollGap);
-        v3 = gran_load(g);
-        // the error word and the watchdog every 8 rounds (32 polls): the error
-        // word's load drains the polls in flight
-        if ((++round & 7u) == 0u) {
-            if (ctrl_load(ctrl + 1) != 0u) return v3;
-            if (__builtin_amdgcn_s_memrealtime() - t0 > tmo) {
-                give_up(ctrl, 1u, site, gp, tag, (int64_t)(v3 >> 32));
-                return v3;
-            }
-        }
-    }
-}
-#endif
 
 // Leading 16-row chunks of a block whose granules all carry `tag` (0 .. 4).
 __device__ __forceinline__ int chunks_ready(uint64_t v, uint32_t tag) {

@@ -64,23 +64,6 @@ constexpr int kG = 4;            // rows per group (one v_perm word): ring / fee
 constexpr int kBatch = 8;        // rows per store-wave batch
 constexpr int kEnt = 16;         // rows per rowpack entry (16 row characters)
 constexpr int kPanelWords = 8;   // per-panel control words (reset with the wave counters)
-// trips (64 rows) at the start / end of a panel whose left values are loaded after
-// the group instead of one group ahead (a wave then trails its producer by one group,
-// not two: a shorter panel-to-panel hop where it sets the ramp, r04v)
-#if defined(NW_ROWS_LATEFEED)
-constexpr int kLateHead = 1 << 30, kLateTail = 0;
-#else
-#ifdef NW_ROWS_LATE_HEAD
-constexpr int kLateHead = NW_ROWS_LATE_HEAD;
-#else
-constexpr int kLateHead = 0;
-#endif
-#ifdef NW_ROWS_LATE_TAIL
-constexpr int kLateTail = NW_ROWS_LATE_TAIL;
-#else
-constexpr int kLateTail = 0;
-#endif
-#endif
 
 // Store waves per compute wave.  Under full HBM load one 1 KB store holds its
 // wave for ~330 cycles (tools/ubench/panel_store: 4 waves x 1 KB per CU reach
@@ -236,7 +219,6 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
             tlo[k] = thi[k] = 0u;
         }
     }
-#ifndef NW_ROWS_CHAIN1
     // T_k[m] = max over k' <= k of max(s'(a_k', char m), tfloor): the prefix of
     // the carry's own contributions (see row() below), one v_perm per 4 rows
     const int32_t tfloor = SW ? gap : 0;
@@ -259,7 +241,6 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
             tthi[k] = hi;
         }
     }
-#endif
 
     // ---- the left column, rows 0 .. : x[r][j0-1]
     //   wave w > 0: wave w-1's last column, read out of w-1's ring;
@@ -349,13 +330,8 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
     // entries ahead into wd[e & 3]
     uint32_t wd[4][4];
     // entries (16 rows each) the row characters are loaded ahead (at most 3: a ring of 4)
-#ifdef NW_ROWS_WPD
-    constexpr int kWPD = NW_ROWS_WPD;
-#else
     constexpr int kWPD = 2;
-#endif
     static_assert(kWPD >= 1 && kWPD <= 3, "");
-#ifndef NW_ROWS_SLOAD
     // a VECTOR load (every lane the same 16 bytes: one request), counted on vmcnt:
     // an s_load shares lgkmcnt with the LDS and returns out of order, so every LDS
     // wait issued while it is in flight is an lgkmcnt(0) that also waits for it
@@ -368,48 +344,8 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
 #pragma unroll
         for (int q = 0; q < 4; ++q) o[q] = v[q];
     };
-#else
-    const cu32 *rq = (const cu32 *)A.rowpack;
-    auto wload = [&](int32_t e, uint32_t (&o)[4]) {
-        const int64_t x0 = ((int64_t)__builtin_amdgcn_readfirstlane(e) * kEnt + kQOff) * 4;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) o[q] = rq[x0 + q];
-    };
-#endif
 
     // ---- one row: x (row r-1) -> x (row r), lv = the left value of row r
-#ifdef NW_ROWS_CHAIN1
-    // ---- one row: x (row r-1) -> x (row r), lv = the left value of row r
-    auto row = [&](uint32_t word, const uint32_t (&pks)[C], const uint32_t (&tks)[C], int q, int32_t lv) {
-        (void)tks;
-        int32_t pfx[C];
-#pragma unroll
-        for (int k = 0; k < C; ++k) {
-            const int32_t dg = k == 0 ? cp : x[k - 1];
-            const int32_t d = dg + sub_score<MODE>(pks[k], word, q, ach[k], msp, mmp);
-            // NW: max(x[r-1][j-1] + s', x[r-1][j]); SW: max(u[r-1][j-1] + s - GAP,
-            // u[r-1][j] + GAP, z_j); then the prefix along the lane, the left value
-            // folded into the last column (so that the lane total carries it)
-            const int32_t m = SW ? max(max(d, x[k] + gap), z[k]) : max(d, x[k]);
-            if (k == 0)
-                pfx[0] = C == 1 ? max(m, lv) : m;
-            else if (k == C - 1)
-                pfx[k] = max(m, max(pfx[k - 1], lv));
-            else
-                pfx[k] = max(m, pfx[k - 1]);
-        }
-        const int32_t S = wave_scan_max(pfx[C - 1]);
-        // exclusive carry: lane l-1's final last column; lane 0: the left value
-        const int32_t carry = __builtin_amdgcn_update_dpp(lv, S, 0x138 /*wave_shr:1*/, 0xF, 0xF, false);
-#pragma unroll
-        for (int k = 0; k < C - 1; ++k) x[k] = max(pfx[k], carry);
-        x[C - 1] = S;
-        cp = carry;
-#pragma unroll
-        for (int k = 0; k < C; ++k) wv[k] = x[k];
-    };
-
-#else
     // ---- one row, the short-chain form.  State: P[k] = the previous row's
     // pre-carry prefixes (P[C-1] including its left value) and cp = its carry
     // into this lane (the final value of column jl-1); its finals are
@@ -463,7 +399,6 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
         wv[C - 1] = S;
         cp = carry;
     };
-#endif
 
     // ---- main loop: trips of 64 rows = 16 groups of kG = 4 rows (compile-time
     // group index, so every register ring above is indexed statically).  Row 0
@@ -477,15 +412,6 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
     if (src != SRC_BOUND) fbv = ctr_load(prod_written);
     const uint64_t tstart = __builtin_amdgcn_s_memrealtime();
     for (int trip = 0; trip < ntrips && !dead; ++trip) {
-        constexpr bool kAnyLate = kLateHead > 0 || kLateTail > 0;
-        const bool late = kAnyLate && (trip < kLateHead || trip >= ntrips - kLateTail);
-#ifdef NW_ROWS_MIDFEED
-        // mid feed: the next group's left values after this group's second row (a
-        // wave trails its producer by 6 rows instead of 8; 2 rows hide the read)
-        constexpr bool kMid = true;
-#else
-        constexpr bool kMid = false;
-#endif
         static_for<0, 16>([&](auto gc) {
             constexpr int g = decltype(gc)::value;
             const int32_t r0 = 64 * trip + kG * g;
@@ -498,16 +424,12 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
 #pragma unroll
             for (int k = 0; k < C; ++k) {
                 pks[k] = PERM ? __builtin_amdgcn_perm(thi[k], tlo[k], word) : 0u;
-#ifndef NW_ROWS_CHAIN1
                 tks[k] = PERM ? __builtin_amdgcn_perm(tthi[k], ttlo[k], word) : 0u;
-#else
-                tks[k] = 0u;
-#endif
             }
             if constexpr ((g & 3) == 0) wload(r0 / kEnt + kWPD, wd[((g >> 2) + kWPD) & 3]);
             // the next group's left values
             const int32_t rn = r0 + kG;
-            if (!kMid && !late && rn < nrow_it) {
+            if (rn < nrow_it) {
                 if (src != SRC_BOUND) ring_feed(rn + kG);
                 feed_load(rn, lvn);
             }
@@ -522,27 +444,15 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
                 } else {
                     *(int4 *)dst = make_int4(wv[0], wv[1], wv[2], wv[3]);
                 }
-                if (kMid && u == 0 && src != SRC_BOUND) fbv = ctr_load(prod_written);
                 if (u == 1) {
-                    if (kMid && rn < nrow_it) {
-                        if (src != SRC_BOUND) ring_feed(rn + kG);
-                        feed_load(rn, lvn);
-                    }
                     // counters for the next group's checks, read mid-group so that
                     // their latency hides behind rows 2 and 3
                     ring_poll();
-                    if (!kMid && src != SRC_BOUND) fbv = ctr_load(prod_written);
+                    if (src != SRC_BOUND) fbv = ctr_load(prod_written);
                 }
             }
             lds_order();
             ctr_store(ctr, r0 + kG);  // rows written
-            // late trips: the next group's left values once this group is out: a wave
-            // then trails its left neighbour by one group instead of two (the read's
-            // LDS latency is exposed at the next group's first row)
-            if (late && rn < nrow_it) {
-                if (src != SRC_BOUND) ring_feed(rn + kG);
-                feed_load(rn, lvn);
-            }
         });
     }
     // every row is in the ring (or the panel is abandoned): release the store
@@ -586,7 +496,6 @@ __device__ __forceinline__ void feeder_in(const FillArgs &A, char *__restrict__ 
     const uint64_t tmo = A.timeout_ticks;
     int32_t avail = 0, consv = 0;
     uint64_t t_last = __builtin_amdgcn_s_memrealtime();
-#ifndef NW_POLL_PIPELINED  // default: one load in flight (A/B r04c: pipelined polls
                             // made the 256k fill 44.9 -> 48.7 ms, nw_dev.h wait_chunk)
     while (avail < nrow_it) {
         // feed-ring space for rows avail .. avail+63
@@ -614,77 +523,6 @@ __device__ __forceinline__ void feeder_in(const FillArgs &A, char *__restrict__ 
             __builtin_amdgcn_s_sleep(1);
         }
     }
-#else
-    // Pipelined: 4 loads of 64 granules in flight, each from the first row not yet
-    // delivered when it was issued (its base b); a load that returns delivers the
-    // leading run of matching rows from `avail` (rows b + lane, lanes avail - b ..)
-    // and is re-issued at the new `avail` after kPollGap.  A granule that becomes
-    // visible is then seen about half a load latency + the gap later instead of
-    // ~1.5 latencies (nw_dev.h wait_chunk).  The error word and the watchdog are
-    // checked every 32 loads without progress (the error word's load drains the
-    // loads in flight).
-    typedef const __attribute__((address_space(1))) uint64_t *gptr;
-    const gptr gg = (gptr)gin;
-    int32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0;
-    uint64_t g0 = gran_load(gg + min(lane, nrow_it - 1));
-    uint64_t g1 = g0, g2 = g0, g3 = g0;
-    bool done = false;
-    uint32_t idle = 0;
-    // one pipeline step on slot (g, b): deliver, then re-issue
-    auto step = [&](uint64_t &g, int32_t &b) {
-        const int32_t k = avail - b;  // lanes below k hold rows already delivered
-        const int32_t r = b + lane;
-        const uint64_t ok = __ballot(r < nrow_it && (uint32_t)(g >> 32) == tag_in);
-        const uint64_t run = k < 64 ? ~(ok >> k) : 0ull;
-        const int n = k >= 64 ? 0 : run == 0ull ? 64 - k : min((int)__builtin_ctzll(run), 64 - k);
-        if (n > 0) {
-            const int32_t need = avail + n - kFeedRows;  // feed-ring space for the new rows
-            if (consv < need) {
-                consv = wait_counter(cons, need, A.ctrl, 16, tmo);
-                if (consv == kDead) {
-                    done = true;
-                    return;
-                }
-            }
-            if (lane >= k && lane < k + n) feed[(uint32_t)r & (kFeedRows - 1)] = (int32_t)(uint32_t)g;
-            lds_order();
-            avail += n;
-            ctr_store(avail_w, avail);
-            t_last = __builtin_amdgcn_s_memrealtime();
-            idle = 0;
-        } else {
-            __builtin_amdgcn_s_sleep(kPollGap);
-            if ((++idle & 31u) == 0u) {
-                if (ctrl_load(A.ctrl + 1) != 0u) {
-                    done = true;
-                    return;
-                }
-                if (__builtin_amdgcn_s_memrealtime() - t_last > tmo) {
-                    give_up(A.ctrl, 1u, 13, gin + min(avail, nrow_it - 1), tag_in, (int64_t)(g >> 32));
-                    done = true;
-                    return;
-                }
-            }
-        }
-        b = avail;
-        g = gran_load(gg + min(avail + lane, nrow_it - 1));
-    };
-    __builtin_amdgcn_s_sleep(kPollGap);
-    g1 = gran_load(gg + min(lane, nrow_it - 1));
-    __builtin_amdgcn_s_sleep(kPollGap);
-    g2 = gran_load(gg + min(lane, nrow_it - 1));
-    __builtin_amdgcn_s_sleep(kPollGap);
-    g3 = gran_load(gg + min(lane, nrow_it - 1));
-    while (!done && avail < nrow_it) {
-        step(g0, b0);
-        if (done || avail >= nrow_it) break;
-        step(g1, b1);
-        if (done || avail >= nrow_it) break;
-        step(g2, b2);
-        if (done || avail >= nrow_it) break;
-        step(g3, b3);
-    }
-#endif
     ctr_store(avail_w, kDone);
 }
 
@@ -861,12 +699,10 @@ __global__ __launch_bounds__((64 * Lay<C, NW>::kWaves)) void nw_fill_panels(Fill
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // issue priority: the compute waves are the latency-bound chain (their
     // partners on a SIMD are store waves, whose stalls are the memory's)
-#ifndef NW_PANEL_NOPRIO
     if (wave < NW)
         __builtin_amdgcn_s_setprio(2);
     else if (wave >= L::kFeedIn)
         __builtin_amdgcn_s_setprio(1);
-#endif
     for (;;) {
         if (threadIdx.x == 0) {
             for (int w = 0; w < L::kPanelWord + kPanelWords; ++w) ctl[w] = 0;  // (the panel words too)

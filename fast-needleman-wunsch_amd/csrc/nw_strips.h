@@ -111,27 +111,16 @@ struct Lay {
     // step); group g = step / 4 of the ring holds the 64 lanes' records, lane l
     // at record slot gpos(l) (grp_pos below)
     static constexpr bool kGrp = C == 1;
-#ifdef NW_SPR
-    static constexpr int kSPR = NW_SPR;  // (tuning builds: make variant DEFS=-DNW_SPR=3)
-#else
-#ifndef NW_SPR2
-#define NW_SPR2 2
-#endif
-    static constexpr int kSPR = C == 4 ? 3 : C == 1 ? 1 : NW_SPR2;
-#endif
-#ifdef NW_BATCH
-    static constexpr int kBatch = NW_BATCH;
-#else
+    static constexpr int kSPR = C == 4 ? 3 : C == 1 ? 1 : 2;
     static constexpr int kBatch = C == 4 ? 8 : 16;
-#endif
     // FEEDER wave (opt-in build NW_FEEDER; one per workgroup, the last): polls the
     // left strip's granules and fills compute wave 0's feed ring + counter (ctl word
     // kFeedWord), so that wave 0 waits on LDS only.  Measured (profiles/
     // r04g_feeder_ab.txt): hop 11.7 -> 8.5 us on the horizontal band, but the band
-    // 32.7 -> 42.1 ms and the SW fill 6.6 -> 7.0 ms -- the workgroup's extra wave
-    // changed the compute waves' code (run_iter 102 -> 140 cycles per step for
-    // strip 0), so it stays off.  Not for shapes whose workgroup would then exceed
-    // 8 waves (register budget).
+    // 32.7 -> 42.1 ms and the SW fill 6.6 -> 7.0 ms: the compute waves then spend
+    // 10 % more cycles per step inside run_iter (profiles/r04s_feeder_cycles.txt), so
+    // it stays off.  Not for shapes whose workgroup would then exceed 8 waves
+    // (register budget).
 #ifdef NW_FEEDER
     static constexpr bool kFeeder = NC * (1 + kSPR) < 8;
 #else
@@ -143,11 +132,7 @@ struct Lay {
     // (the ring's 64 slots of slack are eaten by these granularities: a batch,
     // the check period plus the staleness of the counter it uses, the publish
     // period -- keep them small)
-#ifdef NW_CHK
-    static constexpr int kChk = NW_CHK;
-#else
     static constexpr int kChk = 16;
-#endif
     static constexpr int kPub = 8;
 };
 // Record slot of compute lane a inside a group of a grouped ring: a rotation
@@ -392,12 +377,8 @@ __device__ __forceinline__ void run_iter(char *__restrict__ lds, int it, const u
             constexpr int q = decltype(qc)::value;
             constexpr int u = 4 * g + q;
             const int32_t lf = q == 0 ? fcur.x : q == 1 ? fcur.y : q == 2 ? fcur.z : fcur.w;
-#ifdef NW_EXP_NODPP  // timing experiment only (wrong results): no cross-lane shift
-            int32_t left = S.u[C - 1] + lf;
-#else
             int32_t left = __builtin_amdgcn_update_dpp(lf, S.u[C - 1], 0x138 /*wave_shr:1*/,
                                                        0xF, 0xF, false);
-#endif
             int32_t diag = S.dg;
             S.dg = left;
             // Smith-Waterman: this step's floor -GAP*(i + j) of column 0 (one add per
@@ -440,11 +421,7 @@ __device__ __forceinline__ void run_iter(char *__restrict__ lds, int it, const u
                     set_comp<C>(tv, k, x);
                 }
             });
-#ifdef NW_EXP_NORING  // timing experiment only (wrong results): no ring writes
-            if constexpr (false) {
-#else
             if constexpr (!L::kGrp) {
-#endif
                 *(VT *)(ringw + u * L::kSlot) = tv;  // ring slot 64*HALF + u
             } else if constexpr ((u & 3) == 3) {
                 // group 16*HALF + u/4: this lane's record of steps u-3 .. u
@@ -676,11 +653,7 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
     //   profiles/r04h_step_loop_gpd2.txt); so (4,1) -- the horizontal strips' shape
     //   -- uses 1, the others 3 (the row words' distance).
     constexpr int NB = 4, PD = NB - 1;
-#ifdef NW_GPD
-    constexpr int GPD = NW_GPD;
-#else
     constexpr int GPD = (C == 4 && NC == 1) ? 1 : 3;
-#endif
     static_assert(GPD >= 1 && GPD <= PD, "granule prefetch distance");
     uint64_t gb[NB];
     u32x4 pkb[NB][4];
@@ -882,11 +855,7 @@ __device__ __forceinline__ void feed_strip(const FillArgs &A, char *__restrict__
                     break;
                 }
             }
-#ifdef NW_FEED_SLEEP  // A/B: the poll period of an idle feeder
-            __builtin_amdgcn_s_sleep(NW_FEED_SLEEP);
-#else
             __builtin_amdgcn_s_sleep(1);
-#endif
         }
     }
     ctr_store(avail_w, kDone);  // (also releases wave 0 when the wait gave up: the error word is set)
@@ -1189,11 +1158,7 @@ __device__ __forceinline__ void store_strip_tr(const FillArgs &A, char *__restri
 #pragma unroll
                 for (int e = 0; e < 4; ++e) o[e] = v[blk][e][k] + kf + ug * (uint32_t)(32 * blk + e + k);
                 if (xok && ((rmask >> (4 * blk + k)) & 1u))
-#ifdef NW_TR_NT  // A/B: non-temporal table stores in the horizontal strips
-                    __builtin_nontemporal_store(o, (u32x4 *)(col + (int64_t)(32 * blk + k) * rowb));
-#else
                     *(u32x4 *)(col + (int64_t)(32 * blk + k) * rowb) = o;
-#endif
             }
     }
     ctr_store(mine, kDone);
@@ -1414,9 +1379,8 @@ __device__ __forceinline__ void store_strip_grp(const FillArgs &A, char *__restr
     }
     // Row band: hand this ring's 64 columns of the last row to the next band (see
     // store_strip) -- from the store wave that stored the row's right half, the
-    // later one; with the default kSPR = 1 for C = 1 that wave also stored the
-    // left half (the NW_SPR tuning override with NS > 1 is for timing builds)
-    static_assert(NS == 1 || L::kSPR != 1, "");
+    // later one; with kSPR = 1 for C = 1 that wave also stored the left half
+    static_assert(NS == 1, "one store wave per grouped ring");
     if (B.halo_out != nullptr && ((nrows - 1 + kLagH) / BATCH) % NS == q && ctrl_load(A.ctrl + 1) == 0u) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -1440,45 +1404,6 @@ constexpr bool sw_shape(int c, int nc) {
     return (c == 2 && nc == 2) || (c == 1 && nc == 4) || (c == 4 && nc == 1) || (c == 2 && nc == 1);
 }
 
-// Role of each physical wave.  Roles are logical indices: compute waves 0 .. NC-1,
-// store waves NC .. (NC + b serves ring b % NC), the feeder last.  A workgroup of
-// more than 4 waves puts two on some SIMD (one issue port); with NW_ROLE_RR the
-// compute roles go to the waves that are alone on their SIMD under round-robin
-// placement (SIMD = wave mod 4, tools/ubench/wave_simd.hip), the store roles to
-// the waves that share one.  Default: identity.
-struct RoleOrder {
-    int logical[16];
-    constexpr RoleOrder(int W, bool rr) : logical{} {
-        int order[16] = {};
-        int k = 0;
-        for (int w = 0; w < W; ++w)
-            if (!rr || (w + 4 >= W && w - 4 < 0)) order[k++] = w;
-        if (rr)
-            for (int w = 0; w < W; ++w)
-                if (!(w + 4 >= W && w - 4 < 0)) order[k++] = w;
-        for (int l = 0; l < W; ++l) logical[order[l]] = l;
-    }
-};
-#ifdef NW_ROLE_RR
-constexpr bool kRoleRR = true;
-#else
-constexpr bool kRoleRR = false;
-#endif
-template <int C, int NC>
-__device__ __forceinline__ int role_of(int w) {
-    constexpr RoleOrder R(Lay<C, NC>::kWaves, kRoleRR);
-    if constexpr (!kRoleRR) {
-        return w;
-    } else {
-        int l = 0;
-        static_for<0, Lay<C, NC>::kWaves>([&](auto wc) {
-            constexpr int pw = decltype(wc)::value;
-            if (w == pw) l = R.logical[pw];
-        });
-        return l;
-    }
-}
-
 // Persistent grid of workgroups of NC compute waves (0 .. NC-1) and NC*kSPR
 // store waves (wave NC + b serves ring b % NC).
 template <int C, int NC, bool UNIT>
@@ -1490,12 +1415,7 @@ __global__ __launch_bounds__((64 * Lay<C, NC>::kWaves)) void nw_fill_strips(Fill
     // wave-uniform in an SGPR: every role / feed / output decision below is a
     // scalar branch (a divergent one would run the untaken side's spin-waits
     // with EXEC = 0, where they never see their counter)
-    const int wave = role_of<C, NC>(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));  // (logical role)
-#ifdef NW_COMPUTE_PRIO
-    // compute waves first at a SIMD's issue arbiter (a store wave shares a SIMD with
-    // a compute wave whenever the workgroup has more than 4 waves)
-    if (wave < NC) __builtin_amdgcn_s_setprio(NW_COMPUTE_PRIO);
-#endif
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     for (;;) {
         if (threadIdx.x == 0) {
             for (int w = 0; w < L::kStripWord; ++w) ctl[w] = 0;
