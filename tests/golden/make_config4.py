@@ -11,10 +11,11 @@ tests/golden/config4_524288_shipped.npz:
   score          t[n2][n1] = the score mpi-horz-driver.cpp:88-90 prints (214685)
   rows, first, d every band-boundary row (65536 r - 1 and 65536 r, r = 1..7: each
                  band's halo row and its first computed row; 65536 r - 1 is also
-                 band r-1's last row), row 1, row n2, and seeded rows inside bands 3
-                 and 7 -- whole rows, column 0 + int8 differences along the row
+                 band r-1's last row), row 1, row n2, and seeded rows inside bands 3,
+                 7, 0 and 6 -- whole rows, column 0 + int8 differences along the row
   last_col       t[0..n2][n1], delta-encoded
-  cs_bands       the bands whose every row has checksums: 3 and 7
+  cs_bands       the bands whose every row has checksums: 0, 3, 6 and 7 (round 5
+                 added 0 -- the band with no halo -- and 6, the producer of 7)
   row_sum_<r>,   (sum, (j+1)-weighted sum) mod 2^64 of every row of band r
   row_wsum_<r>   (its halo row included), delta-encoded
 tests/test_config4.py decodes it; a GPU test fills one rank's band alone on one
@@ -32,7 +33,8 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 N, P, SCHEME = 524288, 8, (1, 0, -1)
-CS_BANDS = (3, 7)
+CS_BANDS = (0, 3, 6, 7)
+SEEDED = (3, 7, 0, 6)  # (draw order: round 4's rows for bands 3 and 7 come first, unchanged)
 OUT = os.path.join(HERE, "config4_524288_shipped.npz")
 
 
@@ -49,7 +51,7 @@ def pick_rows():
         _, st = oracle.band_layout(N, P, r)
         want |= {st, st + 1}
     rng = np.random.default_rng(4)
-    for r in CS_BANDS:
+    for r in SEEDED:
         nr, st = oracle.band_layout(N, P, r)
         want |= {int(x) for x in rng.integers(st + 2, st + nr, 6)}
     return np.array(sorted(want), dtype=np.int64)

@@ -13,9 +13,13 @@ The band's own published boundary is captured and compared with the next band's
 halo row, so both ends of the multi-GPU hand-off are checked at full size.
 
 CPU: the fixture decodes consistently (score, boundary rows, sums).
-GPU: ranks 3 and 7 in both sweeps: every row's checksums, the last column, the
-boundary rows and the fixture's rows inside the band cell by cell, the published
-last row, and (rank 7) the final score 214685.
+GPU: ranks 0 (no halo: it seeds row 0 and only publishes), 3 and 7 in both
+sweeps: every row's checksums, the last column, the boundary rows and the
+fixture's rows inside the band cell by cell, the published last row, and (rank
+7) the final score 214685.  And the real hand-off at full size: ranks 6 and 7
+(274.9 GB together, as much as the 256k table) filled CONCURRENTLY on one GPU,
+each on half the CUs, band 6's halo from the fixture and band 7's from band 6's
+kernel, in both sweeps.
 """
 import json
 import os
@@ -97,12 +101,62 @@ def granules(torch, values: np.ndarray, tag: int, size: int):
     return torch.from_numpy(out).cuda()
 
 
+def halo_granules(torch, g, start: int, sweep: str, tag: int):
+    """Band (start)'s halo row from the fixture as its upstream rank's kernel would
+    publish it: raw values (vertical sweep, nw_fill_band_async) or w-form values
+    w = t - GAP (start + j) (horizontal sweep's feed, nw_fill_tband_async)."""
+    row = full_row(g, start)
+    if sweep == "vertical":
+        return granules(torch, row, tag, N + 1)
+    j = np.arange(N + 1, dtype=np.int64)
+    return granules(torch, row.astype(np.int64) - GAP * (j + start), tag, nwhip.feed_bytes(N) // 8)
+
+
+def out_buffer(torch, sweep: str):
+    return torch.zeros(N + 1 if sweep == "vertical" else nwhip.feed_bytes(N) // 8, dtype=torch.int64,
+                       device="cuda")
+
+
+def check_band(torch, g, tab, rank: int):
+    """Band `rank`'s table against the fixture: its first (halo / boundary) and last
+    rows, its last column, every fixture row inside it cell by cell, every row's
+    checksums where the fixture has them, and (last rank) the score."""
+    from test_full_size import row_checksums
+    rows, start = nwhip.band_layout(N, P, rank)
+    want_last = full_row(g, start + rows - 1)
+    np.testing.assert_array_equal(tab[rows - 1, :N + 1].cpu().numpy(), want_last)
+    np.testing.assert_array_equal(tab[:rows, N].cpu().numpy(), g["last_col"][start:start + rows])
+    want_first = full_row(g, start) if start > 0 else GAP * np.arange(N + 1, dtype=np.int32)  # serial.cpp:16
+    np.testing.assert_array_equal(tab[0, :N + 1].cpu().numpy(), want_first)
+    for k, r in enumerate(g["rows"]):
+        if start <= r < start + rows:
+            got = tab[int(r) - start, :N + 1].cpu().numpy()
+            bad = np.flatnonzero(got != g["full"][k])
+            assert bad.size == 0, f"band {rank} row {r}: {bad.size} cells differ, first col {bad[0]}"
+    if rank in g["cs_bands"]:
+        rs, rw = row_checksums(torch, tab, rows, N + 1)
+        bad = np.flatnonzero((rs != g["row_sum"][rank]) | (rw != g["row_wsum"][rank]))
+        assert bad.size == 0, f"band {rank}: {bad.size} rows differ, first {(bad[:5] + start).tolist()}"
+    if rank == P - 1:
+        assert int(tab[rows - 1, N].item()) == g["score"] == 214685
+
+
+def check_published(hout, g, rank: int, sweep: str, tag: int):
+    """What band `rank` published for the next rank: its last row, every granule tagged."""
+    rows, start = nwhip.band_layout(N, P, rank)
+    pub = hout.cpu().numpy()[:N + 1]
+    assert np.all((pub >> 32) == tag)
+    vals = (pub & 0xFFFFFFFF).astype(np.uint32).view(np.int32).astype(np.int64)
+    if sweep == "horizontal":
+        vals = vals + GAP * (np.arange(N + 1, dtype=np.int64) + start + rows - 1)
+    np.testing.assert_array_equal(vals, full_row(g, start + rows - 1))
+
+
 @pytest.mark.gpu
 @pytest.mark.slow
 @pytest.mark.parametrize("sweep", ["vertical", "horizontal"])
-@pytest.mark.parametrize("rank", [3, 7])
+@pytest.mark.parametrize("rank", [0, 3, 7])
 def test_config4_rank_band_alone(torch, g, rank, sweep):
-    from test_full_size import row_checksums
     rows, start = nwhip.band_layout(N, P, rank)
     last = rank == P - 1
     tag = 11
@@ -112,42 +166,68 @@ def test_config4_rank_band_alone(torch, g, rank, sweep):
     try:
         d1 = torch.from_numpy(nwhip.synth(1, N)).cuda()
         d2 = torch.from_numpy(nwhip.synth(2, N)[start:start + rows - 1].copy()).cuda()
-        halo_row = full_row(g, start)
-        j = np.arange(N + 1, dtype=np.int64)
+        hin = halo_granules(torch, g, start, sweep, tag) if rank > 0 else None  # rank 0: row 0 = boundary
+        hout = None if last else out_buffer(torch, sweep)
         if sweep == "vertical":
-            hin = granules(torch, halo_row, tag, N + 1)
-            hout = None if last else torch.zeros(N + 1, dtype=torch.int64, device="cuda")
             ctx.fill_band(d1, d2, tab, halo_in=hin, halo_out=hout, tag=tag, row0=start)
         else:
-            fsize = nwhip.feed_bytes(N) // 8
-            hin = granules(torch, halo_row.astype(np.int64) - GAP * (j + start), tag, fsize)
-            hout = None if last else torch.zeros(fsize, dtype=torch.int64, device="cuda")
             ctx.fill_tband(d1, d2, tab, row0=start, feed_in=hin, feed_out=hout, tag=tag)
         st = ctx.status()
         assert st == nwhip.NW_OK, f"status {st}, first failure {ctx.debug_failure()}"
-        want_last = full_row(g, start + rows - 1)
-        np.testing.assert_array_equal(tab[rows - 1, :N + 1].cpu().numpy(), want_last)
-        np.testing.assert_array_equal(tab[:rows, N].cpu().numpy(), g["last_col"][start:start + rows])
-        np.testing.assert_array_equal(tab[0, :N + 1].cpu().numpy(), halo_row)
-        for k, r in enumerate(g["rows"]):
-            if start <= r < start + rows:
-                got = tab[int(r) - start, :N + 1].cpu().numpy()
-                bad = np.flatnonzero(got != g["full"][k])
-                assert bad.size == 0, f"row {r}: {bad.size} cells differ, first col {bad[0]}"
-        if rank in g["cs_bands"]:
-            rs, rw = row_checksums(torch, tab, rows, N + 1)
-            bad = np.flatnonzero((rs != g["row_sum"][rank]) | (rw != g["row_wsum"][rank]))
-            assert bad.size == 0, f"{bad.size} rows differ, first {(bad[:5] + start).tolist()}"
-        if last:
-            assert int(tab[rows - 1, N].item()) == g["score"] == 214685
-        else:  # what the next rank would receive
-            pub = hout.cpu().numpy()[:N + 1]
-            assert np.all((pub >> 32) == tag)
-            vals = (pub & 0xFFFFFFFF).astype(np.uint32).view(np.int32).astype(np.int64)
-            if sweep == "horizontal":
-                vals = vals + GAP * (j + start + rows - 1)
-            np.testing.assert_array_equal(vals, want_last)
+        check_band(torch, g, tab, rank)
+        if not last:
+            check_published(hout, g, rank, sweep, tag)
     finally:
         del tab
         ctx.close()
+        torch.cuda.empty_cache()
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+@pytest.mark.parametrize("sweep", ["vertical", "horizontal"])
+def test_config4_bands_6_7_handoff(torch, g, sweep):
+    """the producer -> consumer hand-off at config-4 size.  Ranks 6 and 7
+    (65537 + 65538 rows x 524289 = 274.9 GB) run CONCURRENTLY on one GPU, each on
+    its own stream and context with half the resident workers (so both are
+    co-resident and band 7 streams band 6's last row while band 6 still fills);
+    band 6's halo is the fixture's row 393215, band 7's is published by band 6's
+    kernel (the multi-GPU path's protocol, in local memory).  Both bands are
+    checked against the fixture, band 7 through its score 214685."""
+    import nw_bands
+    tag = 13
+    torch.cuda.empty_cache()
+    lay = [nwhip.band_layout(N, P, r) for r in (6, 7)]
+    ctxs = [nwhip.Context(0) for _ in range(2)]
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    tabs = [nwhip.Context.alloc_table(N, rows - 1) for rows, _ in lay]  # 2 x 137 GB
+    try:
+        d1 = torch.from_numpy(nwhip.synth(1, N)).cuda()
+        s2 = nwhip.synth(2, N)
+        d2 = [torch.from_numpy(s2[st:st + rows - 1].copy()).cuda() for rows, st in lay]
+        hin = halo_granules(torch, g, lay[0][1], sweep, tag)
+        link = out_buffer(torch, sweep)  # band 6 -> band 7
+        if sweep == "vertical":
+            waves = max(1, nw_bands.resident_waves(0, *nw_bands.band_shape(N, lay[1][0] - 1)) // 2)
+        else:
+            waves = max(1, nw_bands.resident_waves(0, 4, 1) // 2)
+        torch.cuda.synchronize()
+        for k, ((rows, st), stream) in enumerate(zip(lay, streams)):
+            kw = dict(halo_in=hin if k == 0 else link, halo_out=link if k == 0 else None)
+            if sweep == "vertical":
+                ctxs[k].fill_band(d1, d2[k], tabs[k], tag=tag, row0=st, waves=waves, stream=stream, **kw)
+            else:
+                ctxs[k].fill_tband(d1, d2[k], tabs[k], row0=st, feed_in=kw["halo_in"], feed_out=kw["halo_out"],
+                                   tag=tag, waves=waves, stream=stream)
+        for k, stream in enumerate(streams):
+            st = ctxs[k].status(stream)
+            assert st == nwhip.NW_OK, f"band {6 + k}: status {st}, first failure {ctxs[k].debug_failure()}"
+        torch.cuda.synchronize()
+        check_published(link, g, 6, sweep, tag)
+        check_band(torch, g, tabs[0], 6)
+        check_band(torch, g, tabs[1], 7)
+    finally:
+        del tabs
+        for c in ctxs:
+            c.close()
         torch.cuda.empty_cache()
