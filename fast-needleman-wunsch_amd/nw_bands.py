@@ -16,11 +16,13 @@ waves) with no host round trip and no copy engine, collective or
 stream-ordered gating on the data path.  torch.distributed (gloo) is the control plane
 only: handle exchange, the per-step barrier and the max-over-ranks timing.
 
-An alternate leg sweeps each band in HORIZONTAL strips instead (nw_fill_tband_async:
-256-row strips running along the columns, the halo a feed of one granule per column
-published 16 columns at a time), so that band r+1 starts a strip hop after band r
-rather than after band r's whole height -- measured slower today: a band one row
-over a multiple of 256 rows runs that row as a second pass.
+The bench's `value` sweeps each band in HORIZONTAL strips (nw_fill_tband_async: 256-row
+strips running along the columns, the halo a feed of one granule per column written by
+the band's last strip's store waves), so that band r+1 starts a strip hop after band r
+rather than after band r's whole height; the vertical sweep above, block-cyclic bands and
+column bands run as alternate legs.  Every N > 1 number is the
+per-fill latency of mpi-horz-driver.cpp:38-83 (fill_latencies), with the back-to-back
+throughput reported beside it.
 
 `LocalBands` / `LocalTBands` run P bands concurrently on ONE device (same kernels,
 same halo protocol, local instead of peer memory): an API for band-sized fills and
