@@ -101,7 +101,7 @@ struct Lay {
     // counters, 8 words per compute wave j: [0] steps written, [1] rows of its
     // right column published into wave j+1's feed, [2] iterations done,
     // [3 + q] rows read by its store wave q; then the strip word
-    static constexpr int kCtlWords = 8;
+    static constexpr int kCtlWords = 16;
     static constexpr int kStripWord = NC * kCtlWords;
     static constexpr int kBytes = kCtl + (kStripWord + 4) * 4;
     // store waves per compute wave, rows per store-wave batch (kSPR batches in
@@ -111,7 +111,11 @@ struct Lay {
     // step); group g = step / 4 of the ring holds the 64 lanes' records, lane l
     // at record slot gpos(l) (grp_pos below)
     static constexpr bool kGrp = C == 1;
-    static constexpr int kSPR = C == 4 ? 3 : C == 1 ? 1 : 2;
+#ifndef NW_SPR4
+#define NW_SPR4 5
+#endif
+    static constexpr int kSPR = C == 4 ? NW_SPR4 : C == 1 ? 1 : 2;
+    static_assert(3 + kSPR <= kCtlWords, "counter words per compute wave");
     static constexpr int kBatch = C == 4 ? 8 : 16;
     // FEEDER wave (opt-in build NW_FEEDER; one per workgroup, the last): polls the
     // left strip's granules and fills compute wave 0's feed ring + counter (ctl word
