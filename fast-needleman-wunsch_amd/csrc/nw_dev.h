@@ -61,7 +61,8 @@ __device__ __forceinline__ void ctr_store(int32_t *p, int32_t v) {
 }
 
 // Slow path of the hand-off: re-poll the granules of one 64-row block until
-// those of chunk c (lanes 16c .. 16c+15) carry `tag` (s_sleep between polls).
+// those of chunk c (lanes Gc .. Gc+G-1, G rows per chunk) carry `tag` (s_sleep
+// between polls).
 // Bounded: gives up -- raising the error word -- after `tmo` ticks, or at once
 // if another wave already raised it.  Returns the last value read; the caller
 // re-checks its tag.
@@ -79,11 +80,12 @@ __device__ __forceinline__ void ctr_store(int32_t *p, int32_t v) {
 // same box, profiles/r04c_poll_ab.txt: 256k panels 44.9 -> 48.7 ms, SW 64k strip
 // fill 6.3 -> 7.5 ms: the extra loads of every waiting wave compete with the
 // fill's own traffic.)
+template <int G>
 __device__ __noinline__ uint64_t wait_chunk(const uint64_t *g, uint32_t tag, int c,
                                             uint32_t *ctrl, uint32_t site, uint64_t tmo) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     const int lane = threadIdx.x & 63;
-    const bool in_chunk = (lane >> 4) == c;
+    const bool in_chunk = lane / G == c;
     for (;;) {
         __builtin_amdgcn_s_sleep(1);
         const uint64_t v = gran_load(g);
@@ -96,14 +98,12 @@ __device__ __noinline__ uint64_t wait_chunk(const uint64_t *g, uint32_t tag, int
     }
 }
 
-// Leading 16-row chunks of a block whose granules all carry `tag` (0 .. 4).
+// Leading G-row chunks of a block whose granules all carry `tag` (0 .. 64/G).
+template <int G>
 __device__ __forceinline__ int chunks_ready(uint64_t v, uint32_t tag) {
     const uint64_t ok = __ballot((uint32_t)(v >> 32) == tag);
-    int n = 0;
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-        if (n == c && ((ok >> (16 * c)) & 0xFFFFull) == 0xFFFFull) n = c + 1;
-    return n;
+    const int run = ok == ~0ull ? 64 : (int)__builtin_ctzll(~ok);  // leading tagged rows
+    return run / G;
 }
 
 // Bounded spin until the LDS counter *p reaches `need`; returns the value seen

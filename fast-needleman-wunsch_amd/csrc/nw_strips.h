@@ -111,10 +111,9 @@ struct Lay {
     // step); group g = step / 4 of the ring holds the 64 lanes' records, lane l
     // at record slot gpos(l) (grp_pos below)
     static constexpr bool kGrp = C == 1;
-#ifndef NW_SPR4
-#define NW_SPR4 5
-#endif
-    static constexpr int kSPR = C == 4 ? NW_SPR4 : C == 1 ? 1 : 2;
+    // store waves per compute wave: 5 for C = 4 (3 until round 5, 3 / 5 / 7 measured in
+    // profiles/r05l_store_waves_ab.txt)
+    static constexpr int kSPR = C == 4 ? 5 : C == 1 ? 1 : 2;
     static_assert(3 + kSPR <= kCtlWords, "counter words per compute wave");
     static constexpr int kBatch = C == 4 ? 8 : 16;
     // FEEDER wave (opt-in build NW_FEEDER; one per workgroup, the last): polls the
@@ -138,6 +137,14 @@ struct Lay {
     // period -- keep them small)
     static constexpr int kChk = 16;
     static constexpr int kPub = 8;
+    // rows per published chunk of the right column (granules / LDS feeds); the code
+    // takes 16, 8 or 4.  Finer chunks were slower everywhere (profiles/r05q_gran_ab.txt:
+    // horizontal band 30.4-31.4 -> 33.7 (8) / 42.3 ms (4), its hop 11.6 -> 13.7 / 16.5
+    // us, SW 64k fill 6.19 -> 7.3 / 9.4 ms): a consumer that finds its prefetched block
+    // incomplete pays one poll round trip per chunk, and more chunks per block mean
+    // more of them (feed waits per strip 3.4k -> 5.9k / 12.1k)
+    static constexpr int kGran = 16;
+    static_assert(kGran == 16 || kGran == 8 || kGran == 4, "publish granularity");
 };
 // Record slot of compute lane a inside a group of a grouped ring: a rotation
 // within each 8-lane block, gpos(a) = 8*(a/8) + (a + a/8) % 8.  It keeps both
@@ -258,10 +265,10 @@ struct Lanes {
 enum FeedSrc { FEED_BOUNDARY = 0, FEED_GRAN = 1, FEED_LDS = 2 };
 
 // The feed of one iteration: the left neighbour's right column (w form) for rows
-// 64*it .. 64*it+63, in this wave's LDS feed ring.  `ready` leading 16-row
-// chunks were found there when the iteration started; before the group that
+// 64*it .. 64*it+63, in this wave's LDS feed ring.  `ready` leading chunks of
+// kGran rows were found there when the iteration started; before the group that
 // first reads chunk c >= ready, run_iter waits for it: FEED_GRAN polls the
-// granules (wait_chunk) and writes the 16 values itself, FEED_LDS waits for the
+// granules (wait_chunk) and writes the kGran values itself, FEED_LDS waits for the
 // left compute wave's published-rows counter.
 struct Feed {
     int src;             // FeedSrc (uniform)
@@ -299,9 +306,9 @@ struct Out {
 // latency is hidden).
 //   pk   : row words of this iteration (load_packs), 4 x 16 rows
 //   b    : block whose right column this iteration publishes (it - 1): rows
-//          64b + 16c + i, written by lane 63 at steps 64it + 16c + i - 1, are
-//          read back from the ring by lanes i < 16 after step 16c + 14 and
-//          published three steps later (chunk 3: after the last step)
+//          64b + Gc + i (G = kGran), written by lane 63 at steps 64it + Gc + i - 1,
+//          are read back from the ring by lanes i < G after step Gc + G - 2 and
+//          published three steps later (the last chunk: after the last step)
 //   gp   : this lane's granule of block b (granule output)
 //   F    : the feed of this iteration (chunks not yet there are waited for)
 template <int C, int NC, int MODE, bool RAMP, int HALF>
@@ -324,15 +331,17 @@ __device__ __forceinline__ void run_iter(char *__restrict__ lds, int it, const u
     rbase &= 0x3FFFFu;
     char *ringw = lds + rbase;
     int32_t gq[4];  // grouped rings: results of the current 4-step group
-    // publish chunk c of block b (lanes i < 16 hold rows 64b + 16c + i)
+    constexpr int G = L::kGran;  // rows per chunk
+    constexpr int NCH = 64 / G;  // chunks per block
+    // publish chunk c of block b (lanes i < G hold rows 64b + Gc + i)
     auto publish = [&](int c) {
         if (b < 0 || O.off) return;
         if (O.lds) {
-            if (lane < 16) O.ring[(64 * b + 16 * c + lane) & (kFeedRows - 1)] = S.rcol;
+            if (lane < G) O.ring[(64 * b + G * c + lane) & (kFeedRows - 1)] = S.rcol;
             lds_order();
-            ctr_store(O.pub, 64 * b + 16 * c + 16);
-        } else if (lane < 16) {
-            gran_store(gp + 16 * c, tagw | (uint32_t)S.rcol);
+            ctr_store(O.pub, 64 * b + G * c + G);
+        } else if (lane < G) {
+            gran_store(gp + G * c, tagw | (uint32_t)S.rcol);
         }
     };
     static_for<0, 16>([&](auto gc) {
@@ -350,18 +359,18 @@ __device__ __forceinline__ void run_iter(char *__restrict__ lds, int it, const u
             S.cb = rows_read<L::kSPR>(rd);  // for the next check (kChk steps on)
             lds_order();                    // ring writes after the check
         }
-        // chunk (g+1)/4 is read by the feed load below: wait for it if it was
-        // not there when the iteration started
-        if constexpr ((g & 3) == 3 && g + 1 < 16) {
-            constexpr int c = (g + 1) >> 2;
+        // chunk 4(g+1)/G is read by the feed load below (group g+1 = steps
+        // 4g+4 .. 4g+7): wait for it if it was not there when the iteration started
+        if constexpr ((4 * (g + 1)) % G == 0 && g + 1 < 16) {
+            constexpr int c = 4 * (g + 1) / G;
             if (F.ready <= c) {
                 const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
                 if (F.src == FEED_GRAN) {
-                    const uint64_t v = wait_chunk(F.g, F.tag, c, ctrl, 2, F.tmo);
-                    F.dead |= !__all((lane >> 4) != c || (uint32_t)(v >> 32) == F.tag);
-                    if ((lane >> 4) == c) F.ring[((it & 3) << 6) + lane] = (int32_t)(uint32_t)v;
+                    const uint64_t v = wait_chunk<G>(F.g, F.tag, c, ctrl, 2, F.tmo);
+                    F.dead |= !__all(lane / G != c || (uint32_t)(v >> 32) == F.tag);
+                    if (lane / G == c) F.ring[((it & 3) << 6) + lane] = (int32_t)(uint32_t)v;
                 } else {
-                    F.dead |= wait_counter(F.pub, s0 + 16 * (c + 1), ctrl, 3, F.tmo) == kDead;
+                    F.dead |= wait_counter(F.pub, s0 + G * (c + 1), ctrl, 3, F.tmo) == kDead;
                     lds_order();  // feed reads after the counter that published them
                 }
                 F.nslow += 1;
@@ -431,28 +440,28 @@ __device__ __forceinline__ void run_iter(char *__restrict__ lds, int it, const u
                 // group 16*HALF + u/4: this lane's record of steps u-3 .. u
                 *(int4 *)(ringw + (u >> 2) * (64 * 16)) = make_int4(gq[0], gq[1], gq[2], gq[3]);
             }
-            // right column of block b, chunk c = u / 16: read back after the
+            // right column of block b, chunk c = u / G: read back after the
             // step that completed it (grouped: after its record is written),
             // publish three steps later
-            if constexpr ((u & 15) == (L::kGrp ? 15 : 14)) {
-                constexpr int c = u >> 4;
+            if constexpr (u % G == (L::kGrp ? G - 1 : G - 2)) {
+                constexpr int c = u / G;
                 uint32_t a;
                 if constexpr (L::kGrp) {
-                    // lane i < 16: step 64*HALF + 16c + i - 1 (mod kR) of lane 63
-                    const uint32_t t = (uint32_t)(64 * HALF + 16 * c + (int)S.rc[1]) & (uint32_t)(kR - 1);
+                    // lane i < G: step 64*HALF + Gc + i - 1 (mod kR) of lane 63
+                    const uint32_t t = (uint32_t)(64 * HALF + G * c + (int)S.rc[1]) & (uint32_t)(kR - 1);
                     a = S.rc[0] + (t >> 2) * (64 * 16) + (t & 3u) * 4u;
                 } else {
-                    // lane i < 16: slot (64*HALF + 16c + i - 1) mod kR, lane 63's last column
-                    a = (HALF == 0 && c == 0) ? S.rc[0] : S.rc[1] + (64 * HALF + 16 * c) * L::kSlot;
-                    // (horizontal-strip band: lane a*'s row 64b + 16c + i was written at
-                    // step 64it + 16c + i + a* - 64)
-                    if (S.psel) a = S.pbase + ((uint32_t)(64 * HALF + 16 * c + S.pofs) & (uint32_t)(kR - 1)) * L::kSlot;
+                    // lane i < G: slot (64*HALF + Gc + i - 1) mod kR, lane 63's last column
+                    a = (HALF == 0 && c == 0) ? S.rc[0] : S.rc[1] + (64 * HALF + G * c) * L::kSlot;
+                    // (horizontal-strip band: lane a*'s row 64b + Gc + i was written at
+                    // step 64it + Gc + i + a* - 64)
+                    if (S.psel) a = S.pbase + ((uint32_t)(64 * HALF + G * c + S.pofs) & (uint32_t)(kR - 1)) * L::kSlot;
                 }
                 S.rcol = *(const int32_t *)(lds + a);
             }
-            if constexpr ((u & 15) == (L::kGrp ? 2 : 1) && u > 16) {
-                publish((u >> 4) - 1);
-                if constexpr (u == 16 + (L::kGrp ? 2 : 1)) {
+            if constexpr (u % G == (L::kGrp ? 2 : 1) && u > G) {
+                publish(u / G - 1);
+                if constexpr (u == G + (L::kGrp ? 2 : 1)) {
                     if (F.trace_pub) F.tpub = __builtin_amdgcn_s_memrealtime();
                 }
             }
@@ -462,7 +471,7 @@ __device__ __forceinline__ void run_iter(char *__restrict__ lds, int it, const u
             }
         });
     });
-    publish(3);
+    publish(NCH - 1);
 }
 
 // One strip of a launch: its column strip pk (global: strip0 + k), its place pq
@@ -578,14 +587,14 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
         S.rb[0] = (uint32_t)(j * L::kRing) + (uint32_t)lane * (4u * C);
     }
     S.rb[1] = S.rb[0] + 64u * L::kSlot;
-    // right-column read-back: lane i < 16 reads slot (64*HALF + 16c + i - 1) mod kR
+    // right-column read-back: lane i < G reads slot (64*HALF + Gc + i - 1) mod kR
     // at lane 63's last column (byte kSlot - 4 of the slot).  rc[1] + offset
     // covers every (HALF, c) but (0, 0), whose lane 0 wraps to slot kR - 1: rc[0].
     if constexpr (L::kGrp) {
         S.rc[0] = (uint32_t)(j * L::kRing) + grp_pos(63u) * 16u;
-        S.rc[1] = (uint32_t)((lane & 15) - 1);
+        S.rc[1] = (uint32_t)((lane & (L::kGran - 1)) - 1);
     } else {
-        const int i = lane & 15;
+        const int i = lane & (L::kGran - 1);
         S.rc[1] = (uint32_t)(j * L::kRing + i * L::kSlot - 4);  // (i - 1) * kSlot + kSlot - 4
         S.rc[0] = i == 0 ? (uint32_t)(j * L::kRing + L::kRing - 4) : S.rc[1];
     }
@@ -627,7 +636,7 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
         if (A.tr != 0 && feeds && !O.off) {
             const int as = A.tr_pub / C, ks = A.tr_pub % C;
             S.psel = true;
-            S.pofs = (lane & 15) - 64 + as;
+            S.pofs = (lane & (L::kGran - 1)) - 64 + as;
             S.pbase = (uint32_t)(as * 4 * C + 4 * ks);
         }
     }
@@ -691,33 +700,34 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
         // feed-ring space for this iteration's publish (rows of block it-1 land
         // where rows of block it-5 were): wave j+1 must have finished it-5
         if (O.lds && it >= 5) F.dead |= wait_counter(next_done, it - 4, A.ctrl, 5, A.timeout_ticks) == kDead;
-        F.ready = 4;
+        constexpr int G = L::kGran;
+        F.ready = 64 / G;
         if (it < nblocks) {
             if (F.src == FEED_GRAN) {
                 uint64_t gv = gb[CONS];  // block it, loaded PD iterations ago
                 F.g = gin + (int64_t)it * 64;
-                F.ready = chunks_ready(gv, F.tag);
+                F.ready = chunks_ready<G>(gv, F.tag);
                 if (F.ready == 0) {  // chunk 0 is needed right away
                     const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
                     if (traced) twait = w0;
-                    gv = wait_chunk(F.g, F.tag, 0, A.ctrl, 6, A.timeout_ticks);
-                    F.dead |= !__all((lane >> 4) != 0 || (uint32_t)(gv >> 32) == F.tag);
+                    gv = wait_chunk<G>(F.g, F.tag, 0, A.ctrl, 6, A.timeout_ticks);
+                    F.dead |= !__all(lane >= G || (uint32_t)(gv >> 32) == F.tag);
                     F.nslow += 1;
                     F.wticks += __builtin_amdgcn_s_memrealtime() - w0;
-                    F.ready = max(1, chunks_ready(gv, F.tag));
+                    F.ready = max(1, chunks_ready<G>(gv, F.tag));
                 }
                 F.ring[((it & 3) << 6) + lane] = (int32_t)(uint32_t)gv;
             } else if (F.src == FEED_LDS) {
                 int32_t pv = __builtin_amdgcn_readfirstlane(ctr_load(F.pub));
-                if (pv < it * 64 + 16) {
+                if (pv < it * 64 + G) {
                     const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
                     if (traced) twait = w0;
-                    pv = wait_counter(F.pub, it * 64 + 16, A.ctrl, 7, A.timeout_ticks);
+                    pv = wait_counter(F.pub, it * 64 + G, A.ctrl, 7, A.timeout_ticks);
                     F.dead |= pv == kDead;
                     F.nslow += 1;
                     F.wticks += __builtin_amdgcn_s_memrealtime() - w0;
                 }
-                F.ready = min(4, (pv - it * 64) >> 4);
+                F.ready = min(64 / G, (pv - it * 64) / G);
                 lds_order();  // feed reads after the counter that published them
             } else {
                 // strip 0, wave 0: left of column col0 is the boundary column:
