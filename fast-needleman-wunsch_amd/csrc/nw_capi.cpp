@@ -432,6 +432,13 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
         s.M = std::min<int64_t>(s.nstrips, s.waves + 1);
     }
     if (sw && !panels && !nw::sw_shape_ok(s.K, s.NC)) return NW_ERR_UNSUPPORTED;
+    // (2, 4): half-word rings, Smith-Waterman only, with at most kHalfFixMax cells of
+    // the corner where t may reach 2^16 (nw_sw.hip nw_sw_fixup)
+    const bool half = !panels && s.K == 2 && s.NC == 4;
+    if (half) {
+        int64_t k = 0;
+        if (!sw || nw::sw_half_corner(p->match, p->mismatch, n1, n2, &k) > nw::kHalfFixMax) return NW_ERR_UNSUPPORTED;
+    }
     if (s.nstrips > INT32_MAX / 2 || s.nblocks > INT32_MAX / 2) return NW_ERR_ARG;
 
     int st;
@@ -543,6 +550,10 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
         if (!c->swinfo) NW_HIP_TRY(hipMalloc(&c->swinfo, 16 * sizeof(int64_t)));  // [0..9] traceback info, [12] locate key
         int32_t *best = c->smax + s.nstrips;
         uint64_t *key = (uint64_t *)(c->swinfo + 12);
+        if (half && nw::launch_sw_fixup(d_t, pitch, n1, n2, (const uint8_t *)d_s1, (const uint8_t *)d_s2, p->match,
+                                        p->mismatch, p->gap, col0, (int32_t)(nw::kWave * s.K * s.NC), c->smax,
+                                        stream) != hipSuccess)
+            return NW_ERR_HIP;
         if (nw::launch_sw_locate(d_t, pitch, n1, n2, col0, (int32_t)(nw::kWave * s.K * s.NC), c->smax,
                                  (int32_t)s.nstrips, key, best, stream) != hipSuccess)
             return NW_ERR_HIP;

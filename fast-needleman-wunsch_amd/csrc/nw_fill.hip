@@ -159,7 +159,7 @@ int launch_rowpack(const uint8_t *d_s1, int64_t n1, const uint8_t *d_s2, int64_t
 #define NW_SHAPE(c, nc) true
 #endif
 #define NW_DECL(c, nc) void launch_strips_##c##x##nc(const FillArgs &a, int grid, hipStream_t s);
-NW_DECL(4, 1) NW_DECL(2, 1) NW_DECL(1, 1) NW_DECL(2, 2) NW_DECL(1, 2) NW_DECL(1, 4)
+NW_DECL(4, 1) NW_DECL(2, 1) NW_DECL(1, 1) NW_DECL(2, 2) NW_DECL(1, 2) NW_DECL(1, 4) NW_DECL(2, 4)
 #undef NW_DECL
 
 bool shape_ok(int substrips, int strip_waves) {
@@ -169,6 +169,7 @@ bool shape_ok(int substrips, int strip_waves) {
     switch (substrips * 8 + strip_waves) {
         case 4 * 8 + 1: case 2 * 8 + 1: case 1 * 8 + 1:
         case 2 * 8 + 2: case 1 * 8 + 2: case 1 * 8 + 4:
+        case 2 * 8 + 4:  // (half-word rings: Smith-Waterman only, sw_shape_ok / launch_fill)
             return true;
         default:
             return false;
@@ -182,10 +183,11 @@ bool sw_shape_ok(int substrips, int strip_waves) {
 int launch_fill(const FillArgs &a, int substrips, int strip_waves, int grid, void *stream) {
     hipStream_t s = (hipStream_t)stream;
     if (!shape_ok(substrips, strip_waves)) return (int)hipErrorInvalidValue;
+    if (Lay<2, 4>::kHalf && substrips == 2 && strip_waves == 4 && !a.sw) return (int)hipErrorInvalidValue;
     switch (substrips * 8 + strip_waves) {
 #define NW_CASE(c, nc) \
         case c * 8 + nc: if constexpr (NW_SHAPE(c, nc)) launch_strips_##c##x##nc(a, grid, s); break;
-        NW_CASE(4, 1) NW_CASE(2, 1) NW_CASE(1, 1) NW_CASE(2, 2) NW_CASE(1, 2) NW_CASE(1, 4)
+        NW_CASE(4, 1) NW_CASE(2, 1) NW_CASE(1, 1) NW_CASE(2, 2) NW_CASE(1, 2) NW_CASE(1, 4) NW_CASE(2, 4)
 #undef NW_CASE
         default: return (int)hipErrorInvalidValue;
     }
@@ -199,10 +201,11 @@ int lds_bytes(int substrips, int strip_waves) {
         case 1 * 8 + 1: return Lay<1, 1>::kBytes;
         case 2 * 8 + 2: return Lay<2, 2>::kBytes;
         case 1 * 8 + 2: return Lay<1, 2>::kBytes;
+        case 2 * 8 + 4: return Lay<2, 4>::kBytes;
         default: return Lay<1, 4>::kBytes;
     }
 }
 
-const char *kernel_variant() { return "strips(NCx64xC, compute+store waves, diag ring 128, vperm, gran16, w form) + panels(row scan 4x256, feeder-in/out waves)"; }
+const char *kernel_variant() { return "strips(NCx64xC, compute+store waves, diag ring 128, vperm, gran16, w form; 2x4 half-word SW rings) + panels(row scan 4x256, feeder-in/out waves)"; }
 
 }  // namespace nw

@@ -108,6 +108,16 @@ int launch_tband_edges(const uint64_t *feed, int32_t *table, int64_t pitch, int6
 int launch_sw_locate(const int32_t *table, int64_t pitch, int64_t n1, int64_t n2, int64_t col0,
                      int32_t strip_cols, const int32_t *smax, int32_t nstrips, uint64_t *key, int32_t *best,
                      void *stream);
+// half-word strip rings (Lay::kHalf, Smith-Waterman): the corner i, j >= k whose
+// cells may reach 2^16 (*k = ceil(2^16 / max(match, mismatch))) and its cell count
+int64_t sw_half_corner(int32_t match, int32_t mismatch, int64_t n1, int64_t n2, int64_t *k);
+// cells the host lets the half-word shape leave to nw_sw_fixup (above: refused)
+constexpr int64_t kHalfFixMax = 64;
+// recompute that corner exactly after a half-word fill and raise the strips'
+// best-cell words to its values (asynchronous on `stream`, before launch_sw_locate)
+int launch_sw_fixup(int32_t *table, int64_t pitch, int64_t n1, int64_t n2, const uint8_t *s1, const uint8_t *s2,
+                    int32_t match, int32_t mismatch, int32_t gap, int64_t col0, int32_t strip_cols, int32_t *smax,
+                    void *stream);
 // traceback from (end_i, end_j), parallel over row windows (nw_sw.hip): ops[]
 // gets one byte per move from the end cell back (0 diag, 1 up, 2 left); host
 // info[0] = moves, [1..2] = begin cell, [3] = status (0 ok, 1 ops buffer too

@@ -92,9 +92,16 @@ __device__ __forceinline__ void set_comp(typename Vec<C>::T &v, int k, int32_t x
 
 // LDS of one workgroup: NC rings of kR anti-diagonal slots (64*C int32 each),
 // NC feed rings of kFeedRows int32, the counters.
+//   HALF-WORD rings (kHalf, the (2, 4) shape -- 512-column strips, Smith-Waterman
+// only): a slot holds the low 16 bits of each cell's w, so that four rings fit in
+// 128 KB.  A Smith-Waterman cell satisfies 0 <= t <= max(match, mismatch) *
+// min(i, j), so wherever that bound is below 2^16, t = (w + GAP*(i+j)) mod 2^16 is
+// exact from the low half alone; the host fixes up the corner where it is not
+// (nw_sw.hip nw_sw_fixup) and refuses the shape when that corner is not small.
 template <int C, int NC>
 struct Lay {
-    static constexpr int kSlot = 4 * kWave * C;       // bytes per ring slot
+    static constexpr bool kHalf = C == 2 && NC == 4;
+    static constexpr int kSlot = (kHalf ? 2 : 4) * kWave * C;  // bytes per ring slot
     static constexpr int kRing = kR * kSlot;          // ring bytes (a power of two)
     static constexpr int kFeed = NC * kRing;          // byte offset of the feed rings
     static constexpr int kCtl = kFeed + NC * kFeedRows * 4;
@@ -113,7 +120,7 @@ struct Lay {
     static constexpr bool kGrp = C == 1;
     // store waves per compute wave: 5 for C = 4 (3 until round 5, 3 / 5 / 7 measured in
     // profiles/r05l_store_waves_ab.txt)
-    static constexpr int kSPR = C == 4 ? 5 : C == 1 ? 1 : 2;
+    static constexpr int kSPR = C == 4 ? 5 : C == 1 ? 1 : 2;  // ((2,4): 1 / 3 slower, r05t)
     static_assert(3 + kSPR <= kCtlWords, "counter words per compute wave");
     static constexpr int kBatch = C == 4 ? 8 : 16;
     // FEEDER wave (opt-in build NW_FEEDER; one per workgroup, the last): polls the
@@ -253,6 +260,7 @@ struct Lanes {
     uint32_t rc[2];    // read-back address of the right column (see run_iter); grouped
                        // rings: rc[0] = record of lane 63, rc[1] = (lane & 15) - 1
     int32_t rcol;      // right-column value read back, published a few steps later
+    uint32_t kcol;     // half-word rings: GAP * (the wave's last column), to rebuild w
     // horizontal-strip band, last strip: the published column is the band's last
     // row, compute lane a* / column k* (FillArgs::tr_pub) instead of lane 63's
     // last column: read back from slot (64*HALF + 16c + pofs) mod kR at pbase
@@ -434,7 +442,11 @@ __device__ __forceinline__ void run_iter(char *__restrict__ lds, int it, const u
                     set_comp<C>(tv, k, x);
                 }
             });
-            if constexpr (!L::kGrp) {
+            if constexpr (L::kHalf) {
+                // low halves of the lane's two cells in one dword (v_perm)
+                *(uint32_t *)(ringw + u * L::kSlot) =
+                    __builtin_amdgcn_perm((uint32_t)tv[1], (uint32_t)tv[0], 0x05040100u);
+            } else if constexpr (!L::kGrp) {
                 *(VT *)(ringw + u * L::kSlot) = tv;  // ring slot 64*HALF + u
             } else if constexpr ((u & 3) == 3) {
                 // group 16*HALF + u/4: this lane's record of steps u-3 .. u
@@ -457,7 +469,15 @@ __device__ __forceinline__ void run_iter(char *__restrict__ lds, int it, const u
                     // step 64it + Gc + i + a* - 64)
                     if (S.psel) a = S.pbase + ((uint32_t)(64 * HALF + G * c + S.pofs) & (uint32_t)(kR - 1)) * L::kSlot;
                 }
-                S.rcol = *(const int32_t *)(lds + a);
+                if constexpr (L::kHalf) {
+                    // lane 63's dword: the wave's last column in its high half; the
+                    // cell is t = (w16 + GAP*(i+j)) mod 2^16 (Lay::kHalf), w = t - GAP*(i+j)
+                    const uint32_t kc = S.kcol + (uint32_t)gap * (uint32_t)(64 * b + G * c + (lane & (G - 1)));
+                    const uint32_t t = ((*(const uint32_t *)(lds + a) >> 16) + kc) & 0xFFFFu;
+                    S.rcol = (int32_t)(t - kc);
+                } else {
+                    S.rcol = *(const int32_t *)(lds + a);
+                }
             }
             if constexpr (u % G == (L::kGrp ? 2 : 1) && u > G) {
                 publish(u / G - 1);
@@ -584,8 +604,9 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
     if constexpr (L::kGrp) {
         S.rb[0] = (uint32_t)(j * L::kRing) + grp_pos((uint32_t)lane) * 16u;
     } else {
-        S.rb[0] = (uint32_t)(j * L::kRing) + (uint32_t)lane * (4u * C);
+        S.rb[0] = (uint32_t)(j * L::kRing) + (uint32_t)lane * (uint32_t)(L::kSlot / kWave);
     }
+    S.kcol = (uint32_t)gap * (uint32_t)(c0 + 64 * C - 1);
     S.rb[1] = S.rb[0] + 64u * L::kSlot;
     // right-column read-back: lane i < G reads slot (64*HALF + Gc + i - 1) mod kR
     // at lane 63's last column (byte kSlot - 4 of the slot).  rc[1] + offset
@@ -949,7 +970,7 @@ __device__ __forceinline__ void store_strip(const FillArgs &A, char *__restrict_
 #pragma unroll
     for (int m = 0; m < NR; ++m) {
         const int a = NR * cq + m;
-        pa[m] = (uint32_t)((f0 + ro + a) % kR) * L::kSlot + (uint32_t)a * (4u * C);
+        pa[m] = (uint32_t)((f0 + ro + a) % kR) * L::kSlot + (uint32_t)a * (uint32_t)(L::kSlot / kWave);
     }
     // `rows` further down the ring (the piece offset a * 4C < kSlot survives the mask)
     auto adv = [&](uint32_t x, uint32_t rows) { return (x + rows * L::kSlot) & kMask; };
@@ -979,11 +1000,20 @@ __device__ __forceinline__ void store_strip(const FillArgs &A, char *__restrict_
         for (int g = 0; g < NG; ++g) {
 #pragma unroll
             for (int m = 0; m < NR; ++m) {
-                const VT x = *(const VT *)(ring + pa[m]);
-                pa[m] = adv(pa[m], NR);
+                if constexpr (L::kHalf) {
+                    // two cells' low halves: t = (w16 + GAP*(i+j)) mod 2^16 (Lay::kHalf)
+                    const uint32_t x = *(const uint32_t *)(ring + pa[m]);
+                    pa[m] = adv(pa[m], NR);
 #pragma unroll
-                for (int k = 0; k < C; ++k)
-                    v[g][m * C + k] = (uint32_t)comp<C>(x, k) + kc[m * C + k] + ug * (uint32_t)(g * NR);
+                    for (int k = 0; k < C; ++k)
+                        v[g][m * C + k] = (((k == 0 ? x : x >> 16) + kc[m * C + k] + ug * (uint32_t)(g * NR)) & 0xFFFFu);
+                } else {
+                    const VT x = *(const VT *)(ring + pa[m]);
+                    pa[m] = adv(pa[m], NR);
+#pragma unroll
+                    for (int k = 0; k < C; ++k)
+                        v[g][m * C + k] = (uint32_t)comp<C>(x, k) + kc[m * C + k] + ug * (uint32_t)(g * NR);
+                }
             }
         }
 #pragma unroll
@@ -1415,7 +1445,8 @@ __device__ __forceinline__ void store_strip_grp(const FillArgs &A, char *__restr
 // Strip shapes built with the Smith-Waterman modes (the tuned ones; the others
 // refuse SW launches in nw_capi.cpp) -- each mode is a full copy of the loop.
 constexpr bool sw_shape(int c, int nc) {
-    return (c == 2 && nc == 2) || (c == 1 && nc == 4) || (c == 4 && nc == 1) || (c == 2 && nc == 1);
+    return (c == 2 && nc == 2) || (c == 1 && nc == 4) || (c == 4 && nc == 1) || (c == 2 && nc == 1) ||
+           (c == 2 && nc == 4);
 }
 
 // Persistent grid of workgroups of NC compute waves (0 .. NC-1) and NC*kSPR
@@ -1454,7 +1485,9 @@ __global__ __launch_bounds__((64 * Lay<C, NC>::kWaves)) void nw_fill_strips(Fill
                     sw_done = true;
                 }
             }
-            if (sw_done) {
+            if constexpr (L::kHalf) {
+                // half-word rings hold Smith-Waterman cells only (the host refuses NW)
+            } else if (sw_done) {
             } else if (A.perm != 0 && np <= kMaxPerm) {
                 compute_strip<C, NC, SUB_PERM>(A, lds, B, wave, lane);
             } else if (UNIT) {
@@ -1483,7 +1516,9 @@ __global__ __launch_bounds__((64 * Lay<C, NC>::kWaves)) void nw_fill_strips(Fill
 template <int C, int NC>
 static void launch_c(const FillArgs &a, int grid, hipStream_t s) {
     const dim3 block(64 * Lay<C, NC>::kWaves);
-    if (a.match - a.mismatch == 1 && !a.sw)
+    if constexpr (Lay<C, NC>::kHalf)  // (Smith-Waterman only)
+        hipLaunchKernelGGL((nw_fill_strips<C, NC, false>), dim3(grid), block, 0, s, a);
+    else if (a.match - a.mismatch == 1 && !a.sw)
         hipLaunchKernelGGL((nw_fill_strips<C, NC, true>), dim3(grid), block, 0, s, a);
     else
         hipLaunchKernelGGL((nw_fill_strips<C, NC, false>), dim3(grid), block, 0, s, a);

@@ -90,6 +90,56 @@ int launch_sw_locate(const int32_t *table, int64_t pitch, int64_t n1, int64_t n2
     return (int)hipGetLastError();
 }
 
+// Half-word strip rings (nw_strips.h Lay::kHalf): a Smith-Waterman cell obeys
+// 0 <= t <= M * min(i, j), M = max(match, mismatch) (t[i][0] = t[0][j] = 0 and
+// each move adds at most M), so the rings' t mod 2^16 is exact wherever
+// M * min(i, j) < 2^16.  The rest is the corner i, j >= K = ceil(2^16 / M) (one
+// cell at 65536^2 with match 1): a wrong value there reaches only cells of the
+// same corner (each cell's neighbours up/left/diag of a corner cell are in it or
+// exact), and every value the strips produced there is <= the true one (max-plus
+// with inputs <= the true ones, then the 0 floor and the wrap).  So the corner is
+// recomputed here, in row-major order from its exact upper and left borders, and
+// the strips' best-cell words raised to its true values; the host refuses the
+// half-word shape when the corner exceeds kHalfFixMax cells.
+__global__ __launch_bounds__(64) void nw_sw_fixup(int32_t *__restrict__ t, int64_t pitch,
+                                                  const uint8_t *__restrict__ s1, const uint8_t *__restrict__ s2,
+                                                  int32_t match, int32_t mismatch, int32_t gap, int64_t i0,
+                                                  int64_t i1, int64_t j0, int64_t j1, int64_t col0, int32_t width,
+                                                  int32_t *__restrict__ smax) {
+    if (threadIdx.x != 0) return;
+    for (int64_t i = i0; i <= i1; ++i) {
+        int32_t left = t[i * pitch + j0 - 1];
+        for (int64_t j = j0; j <= j1; ++j) {
+            const int32_t d = t[(i - 1) * pitch + j - 1], u = t[(i - 1) * pitch + j];
+            const int32_t sc = s1[j - 1] == s2[i - 1] ? match : mismatch;
+            const int32_t v = max(max(0, d + sc), max(u + gap, left + gap));
+            t[i * pitch + j] = v;
+            left = v;
+            atomicMax(smax + (j - col0) / width, v);
+        }
+    }
+}
+
+int64_t sw_half_corner(int32_t match, int32_t mismatch, int64_t n1, int64_t n2, int64_t *k) {
+    const int64_t m = std::max(match, mismatch);
+    if (m <= 0) {
+        *k = INT64_MAX;
+        return 0;
+    }
+    *k = (65536 + m - 1) / m;
+    return std::max<int64_t>(0, n2 - *k + 1) * std::max<int64_t>(0, n1 - *k + 1);
+}
+
+int launch_sw_fixup(int32_t *table, int64_t pitch, int64_t n1, int64_t n2, const uint8_t *s1, const uint8_t *s2,
+                    int32_t match, int32_t mismatch, int32_t gap, int64_t col0, int32_t strip_cols, int32_t *smax,
+                    void *stream) {
+    int64_t k = 0;
+    if (sw_half_corner(match, mismatch, n1, n2, &k) == 0) return (int)hipSuccess;
+    hipLaunchKernelGGL(nw_sw_fixup, dim3(1), dim3(64), 0, (hipStream_t)stream, table, pitch, s1, s2, match,
+                       mismatch, gap, k, n2, k, n1, col0, strip_cols, smax);
+    return (int)hipGetLastError();
+}
+
 // Traceback, parallel over windows.  The path from the best cell runs up and
 // left through cells with t > 0, taking at every cell the first move that
 // reproduces t (diag, then up, then left -- the order of serial.cpp:24-30's max).

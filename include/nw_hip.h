@@ -66,7 +66,10 @@ enum {
  *   STRIPS: a wave holds an ANTI-DIAGONAL of a 64*C-column strip (lane = row
  *           offset; DPP carries the left neighbour), rows leave through a
  *           128-slot LDS ring.  Shapes (substrips C, strip_waves NC): (4,1)
- *           (2,1) (1,1) (2,2) (1,2) (1,4).
+ *           (2,1) (1,1) (2,2) (1,2) (1,4); and (2,4), Smith-Waterman only: 512-
+ *           column strips on half-word rings, refused (NW_ERR_UNSUPPORTED) when
+ *           more than 64 cells could reach 2^16 (max(match, mismatch) * min(i, j)
+ *           >= 65536), which are then recomputed exactly after the fill.
  *   PANELS: a wave holds a ROW of 64*C columns, computed as a prefix maximum
  *           (lane-local prefix + a 64-lane DPP max-scan) in the w form; rows
  *           leave through a 32-row ring.  Shapes (C, NW compute waves per
@@ -89,7 +92,8 @@ typedef struct nw_params {
     int32_t substrips; /* columns per lane C of a compute wave (1, 2 or 4); 0 = auto */
     int32_t strip_waves; /* chained compute waves per strip NC (1, 2 or 4); 0 = auto.
                             A strip is NC * 64 * C columns; supported (C, NC):
-                            (4,1) (2,1) (1,1) (2,2) (1,2) (1,4); auto = the tuned
+                            (4,1) (2,1) (1,1) (2,2) (1,2) (1,4), SW also (2,4)
+                            (see NW_KERNEL_AUTO); auto = the tuned
                             shape for the size (nw_tuned_shape) */
     int32_t timeout_ms;  /* bound of every in-kernel wait (hand-off, halo, ring);
                             0 = 20000.  A wait that expires makes the fill return

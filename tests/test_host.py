@@ -62,8 +62,9 @@ def test_pitch_and_bytes():
 
 
 def test_strip_shapes_lds():
-    """Every supported strip shape fits a CU's 160 KiB of LDS; others are refused."""
-    for c, nc in [(4, 1), (2, 1), (1, 1), (2, 2), (1, 2), (1, 4)]:
+    """Every supported strip shape fits a CU's 160 KiB of LDS; others are refused.
+    (2, 4) fits only with its half-word rings (Smith-Waterman only)."""
+    for c, nc in [(4, 1), (2, 1), (1, 1), (2, 2), (1, 2), (1, 4), (2, 4)]:
         b = nwhip.strip_lds_bytes(c, nc)
         assert 0 < b <= 160 * 1024, (c, nc, b)
     assert nwhip.strip_lds_bytes(4, 2) == -1 and nwhip.strip_lds_bytes(3, 1) == -1

@@ -9,7 +9,8 @@ diag > up > left (the order of serial.cpp:24-30's max).
 
 CPU: the two restatements agree (tables, best cell, ops); the golden file is
 self-consistent.  GPU: device tables bit-exact vs the oracle for every SW strip
-shape; nw_sw_align against the golden vectors (bdna pairs, and the 65536 x 65536
+shape (the (2, 4) half-word rings also where cells reach 2^16, through the corner
+fix-up); nw_sw_align against the golden vectors (bdna pairs, and the 65536 x 65536
 synthetic workload = config 5) including the ops' sha256; the score of the
 returned path equals the table maximum (a size-independent property).
 """
@@ -25,7 +26,7 @@ import oracle
 from conftest import GOLDEN
 
 SCHEMES = [(1, -1, -1), (1, 0, -1), (2, -1, -2)]
-SW_SHAPES = [(2, 2), (1, 4), (4, 1), (2, 1)]
+SW_SHAPES = [(2, 2), (1, 4), (4, 1), (2, 1), (2, 4)]  # (2, 4): 512-column strips, half-word rings
 
 
 def sw_golden():
@@ -204,3 +205,55 @@ def test_sw_refusals(torch, ctx):
     with pytest.raises(nwhip.NwError) as e:
         nwhip.sw_align(s, s, (1, -1, 1))
     assert e.value.status == nwhip.NW_ERR_ARG
+
+
+def _half_word_pair(n, mutate, seed):
+    rng = np.random.default_rng(seed)
+    s1 = rng.integers(1, 5, n).astype(np.int8)
+    s2 = s1.copy()
+    pos = rng.random(n) < mutate
+    s2[pos] = (s2[pos] % 4) + 1  # a different character
+    return s1, s2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,mutate", [(660, 0.0), (661, 0.03), (700, 0.0)])
+def test_sw_half_word_corner(torch, ctx, n, mutate):
+    """(2, 4) keeps the low 16 bits of each cell in its LDS rings (nw_strips.h
+    Lay::kHalf).  With match 100 the cells with min(i, j) >= 656 may reach 2^16
+    (identical sequences: up to 66000 at n = 660); that corner -- 25 / 36 cells
+    here -- is recomputed exactly after the fill (nw_sw.hip nw_sw_fixup), so the
+    whole table, the best cell and the path equal the oracle's.  At n = 700 the
+    corner (45 x 45 cells) exceeds the fix-up's bound: refused, and the auto shape
+    still fills it exactly."""
+    scheme = (100, -100, -1)
+    s1, s2 = _half_word_pair(n, mutate, n)
+    d1, d2 = torch.from_numpy(s1).cuda(), torch.from_numpy(s2).cuda()
+    tab = nwhip.Context.alloc_table(n, n)
+    want = oracle.sw_fill(s1, s2, scheme)
+    if n == 700:
+        assert want.max() >= 65536
+        with pytest.raises(nwhip.NwError) as e:
+            ctx.fill(d1, d2, tab, scheme, substrips=2, strip_waves=4, mode=nwhip.MODE_SW)
+        assert e.value.status == nwhip.NW_ERR_UNSUPPORTED
+        r = ctx.fill(d1, d2, tab, scheme, mode=nwhip.MODE_SW)
+    else:
+        assert (want.max() >= 65536) == (mutate == 0.0)
+        tab.fill_(-0x5A5A5A5)
+        r = ctx.fill(d1, d2, tab, scheme, substrips=2, strip_waves=4, mode=nwhip.MODE_SW)
+    np.testing.assert_array_equal(tab[:n + 1, :n + 1].cpu().numpy(), want)
+    assert (r.score, r.end_i, r.end_j) == oracle.sw_best(s1, s2, scheme)
+    al, ops = ctx.sw_traceback(d1, d2, tab, (r.end_i, r.end_j), scheme)
+    wops, bi, bj = oracle.sw_traceback(s1, s2, want, (r.end_i, r.end_j), scheme)
+    np.testing.assert_array_equal(ops, wops)
+
+
+@pytest.mark.gpu
+def test_sw_half_word_shape_is_sw_only(torch, ctx):
+    """The half-word rings hold Smith-Waterman cells only: an NW fill with (2, 4) is
+    refused rather than wrapped."""
+    s = torch.from_numpy(nwhip.synth(1, 2000)).cuda()
+    tab = nwhip.Context.alloc_table(2000, 2000)
+    with pytest.raises(nwhip.NwError) as e:
+        ctx.fill(s, s, tab, (1, 0, -1), substrips=2, strip_waves=4)
+    assert e.value.status == nwhip.NW_ERR_UNSUPPORTED
