@@ -214,7 +214,10 @@ bool valid_params(const nw_params *p) {
     if (p->timeout_ms < 0) return false;
     // known flag bits only; the debug probes leave the table unwritten, so only with TIMING_ONLY
     const int32_t dbg = NW_FLAG_DEBUG_DRAIN | NW_FLAG_DEBUG_NO_STORE;
-    if ((p->flags & ~(NW_FLAG_TIMING_ONLY | NW_FLAG_NO_PROFILE | NW_FLAG_NO_FINISH | dbg)) != 0) return false;
+    if ((p->flags & ~(NW_FLAG_TIMING_ONLY | NW_FLAG_NO_PROFILE | NW_FLAG_NO_FINISH | NW_FLAG_DEBUG_NO_CHAIN |
+                      NW_FLAG_DEBUG_STAGGER | dbg)) != 0)
+        return false;
+    if ((p->flags & NW_FLAG_DEBUG_STAGGER) && !(p->flags & NW_FLAG_DEBUG_NO_CHAIN)) return false;
     if ((p->flags & dbg) != 0 && (p->flags & NW_FLAG_TIMING_ONLY) == 0) return false;
     // keep every intermediate far from int32 overflow (|score| < 2^29)
     const int32_t lim = 1 << 12;
@@ -369,6 +372,7 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
     if (!valid_params(p)) return NW_ERR_ARG;
     const bool sw = p->mode == NW_MODE_SW;
     if (sw && (band || cb)) return NW_ERR_UNSUPPORTED;  // (local alignment: single table, config 5)
+    if ((p->flags & NW_FLAG_DEBUG_NO_CHAIN) && (band || cb)) return NW_ERR_ARG;  // (no fill to hand on)
     if (band && cb) return NW_ERR_ARG;
     // The kernels hold w = t - GAP*(i+j) in int32 next to a "minus infinity" of
     // -2^29: |w| <= (max|score| + |GAP|) * (i + j) must stay below 2^28, with i the
@@ -421,6 +425,7 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
     if (!shape_valid(s)) return NW_ERR_ARG;
     const bool panels = s.kernel == NW_KERNEL_PANELS;
     if (cy && panels) return NW_ERR_UNSUPPORTED;  // (block cycles: the strip kernel)
+    if (panels && (p->flags & NW_FLAG_DEBUG_NO_CHAIN)) return NW_ERR_ARG;  // (a strip-kernel probe)
     if ((int64_t)s.nstrips * nbl > INT32_MAX / 2) return NW_ERR_ARG;
     if (nbl > 1) {  // the launch's chain of hand-offs is nstrips * nbl tickets long
         s.waves = std::max<int64_t>(1, std::min<int64_t>(s.waves_max, s.nstrips * nbl));
@@ -655,6 +660,7 @@ int nw_fill_tband_async(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t 
     if (tb->tag == 0 || (((uintptr_t)tb->feed_in | (uintptr_t)tb->feed_out) & 7u) != 0) return NW_ERR_ARG;
     if ((tb->row0 > 0) != (tb->feed_in != nullptr)) return NW_ERR_ARG;
     if (tb->feed_out && (p->flags & 1)) return NW_ERR_ARG;  // needs the real last row
+    if ((p->flags & NW_FLAG_DEBUG_NO_CHAIN) && (tb->feed_in || tb->feed_out)) return NW_ERR_ARG;  // (no fill to hand on)
     if ((((uintptr_t)d_t + 4u) & 255u) != 0 || pitch % nw::kWave != 0 || pitch < n1 + 4) return NW_ERR_ARG;
     {  // |w| bound of launch_fill, with the global row
         const long long m = std::max({std::llabs(p->match), std::llabs(p->mismatch), std::llabs(p->gap)});

@@ -79,21 +79,29 @@ __device__ __forceinline__ void ctr_store(int32_t *p, int32_t v) {
 // measured a pipelined poll -- 4 loads in flight per waiting wave -- SLOWER on the
 // same box, profiles/r04c_poll_ab.txt: 256k panels 44.9 -> 48.7 ms, SW 64k strip
 // fill 6.3 -> 7.5 ms: the extra loads of every waiting wave compete with the
-// fill's own traffic.)
-template <int G>
+// fill's own traffic.)  The error word and the watchdog are checked every
+// kPollCheck polls only: every waiting wave of the chip re-reading the one error
+// word after each poll made it a hot line and doubled each poll's round trip
+// (round 5: profiles/r05w_poll_split.txt).  The loads are global (the generic
+// pointer of a noinline callee would make them flat loads).
+constexpr uint32_t kPollCheck = 32;
+template <int G, int SLEEP>
 __device__ __noinline__ uint64_t wait_chunk(const uint64_t *g, uint32_t tag, int c,
                                             uint32_t *ctrl, uint32_t site, uint64_t tmo) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     const int lane = threadIdx.x & 63;
     const bool in_chunk = lane / G == c;
-    for (;;) {
-        __builtin_amdgcn_s_sleep(1);
-        const uint64_t v = gran_load(g);
+    const __attribute__((address_space(1))) uint64_t *gg = (const __attribute__((address_space(1))) uint64_t *)g;
+    for (uint32_t n = 1;; ++n) {
+        __builtin_amdgcn_s_sleep(SLEEP);
+        const uint64_t v = gran_load(gg);
         if (__all(!in_chunk || (uint32_t)(v >> 32) == tag)) return v;
-        if (ctrl_load(ctrl + 1) != 0u) return v;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > tmo) {
-            give_up(ctrl, 1u, site, g, tag, (int64_t)(v >> 32));
-            return v;
+        if (n % kPollCheck == 0u) {
+            if (ctrl_load(ctrl + 1) != 0u) return v;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > tmo) {
+                give_up(ctrl, 1u, site, g, tag, (int64_t)(v >> 32));
+                return v;
+            }
         }
     }
 }

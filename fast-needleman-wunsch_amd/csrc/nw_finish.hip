@@ -65,7 +65,7 @@ __device__ __noinline__ int32_t look_back(const uint64_t *look, int32_t k, uint3
     int32_t carry = kNeg;
     int32_t j = k - 1;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    for (;;) {
+    for (uint32_t n = 1;; ++n) {
         const int32_t idx = j - lane;
         const uint64_t g = idx >= 0 ? gran_load(look + idx) : ((uint64_t)tag_inc << 32);
         const uint32_t tg = (uint32_t)(g >> 32);
@@ -80,10 +80,12 @@ __device__ __noinline__ int32_t look_back(const uint64_t *look, int32_t k, uint3
             continue;
         }
         __builtin_amdgcn_s_sleep(1);
-        if (ctrl_load(ctrl + 1) != 0u) return kDead;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > tmo) {
-            give_up(ctrl, 1u, 30, look + max(j, 0), tag_agg, (int64_t)j);
-            return kDead;
+        if (n % kPollCheck == 0u) {  // (the error word: not a hot line, nw_dev.h wait_chunk)
+            if (ctrl_load(ctrl + 1) != 0u) return kDead;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > tmo) {
+                give_up(ctrl, 1u, 30, look + max(j, 0), tag_agg, (int64_t)j);
+                return kDead;
+            }
         }
     }
 }

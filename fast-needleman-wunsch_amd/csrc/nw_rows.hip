@@ -153,6 +153,7 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
     int32_t bnd0 = 0;
     if (A.halo_in != nullptr) {
         const uint64_t h0 = __builtin_amdgcn_s_memrealtime();
+        uint32_t npoll = 0;
         for (;;) {
             bool ok = true;
 #pragma unroll
@@ -169,11 +170,13 @@ __device__ __forceinline__ void compute_panel(const FillArgs &A, char *__restric
             bnd0 = (int32_t)(uint32_t)g0;
             ok &= (uint32_t)(gl >> 32) == A.halo_tag && (uint32_t)(g0 >> 32) == A.halo_tag;
             if (__all(ok)) break;
-            if (ctrl_load(A.ctrl + 1) != 0u) { dead = true; break; }
-            if (__builtin_amdgcn_s_memrealtime() - h0 > tmo) {
-                give_up(A.ctrl, 2u, 4, A.halo_in, A.halo_tag, 0);
-                dead = true;
-                break;
+            if (++npoll % kPollCheck == 0u) {  // (the error word: not a hot line, nw_dev.h wait_chunk)
+                if (ctrl_load(A.ctrl + 1) != 0u) { dead = true; break; }
+                if (__builtin_amdgcn_s_memrealtime() - h0 > tmo) {
+                    give_up(A.ctrl, 2u, 4, A.halo_in, A.halo_tag, 0);
+                    dead = true;
+                    break;
+                }
             }
             __builtin_amdgcn_s_sleep(4);
         }
@@ -495,6 +498,7 @@ __device__ __forceinline__ void feeder_in(const FillArgs &A, char *__restrict__ 
     const int32_t nrow_it = 64 * A.nblocks;
     const uint64_t tmo = A.timeout_ticks;
     int32_t avail = 0, consv = 0;
+    uint32_t npoll = 0;
     uint64_t t_last = __builtin_amdgcn_s_memrealtime();
                             // made the 256k fill 44.9 -> 48.7 ms, nw_dev.h wait_chunk)
     while (avail < nrow_it) {
@@ -515,10 +519,13 @@ __device__ __forceinline__ void feeder_in(const FillArgs &A, char *__restrict__ 
             ctr_store(avail_w, avail);
             t_last = __builtin_amdgcn_s_memrealtime();
         } else {
-            if (ctrl_load(A.ctrl + 1) != 0u) break;
-            if (__builtin_amdgcn_s_memrealtime() - t_last > tmo) {
-                give_up(A.ctrl, 1u, 13, gin + min(avail, nrow_it - 1), tag_in, (int64_t)(g >> 32));
-                break;
+            // the error word and the watchdog every kPollCheck empty polls (nw_dev.h wait_chunk)
+            if (++npoll % kPollCheck == 0u) {
+                if (ctrl_load(A.ctrl + 1) != 0u) break;
+                if (__builtin_amdgcn_s_memrealtime() - t_last > tmo) {
+                    give_up(A.ctrl, 1u, 13, gin + min(avail, nrow_it - 1), tag_in, (int64_t)(g >> 32));
+                    break;
+                }
             }
             __builtin_amdgcn_s_sleep(1);
         }

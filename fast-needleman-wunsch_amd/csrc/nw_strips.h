@@ -269,6 +269,17 @@ struct Lanes {
     uint32_t pbase;
 };
 
+// s_sleep (x 64 clocks) between a waiting compute wave's granule polls in a
+// horizontal-strip band (FillArgs::tr; 1 elsewhere).  Every poll is a system-scope
+// load of a line its producer is writing through; 255 followers polling every
+// ~2 us slowed the band's LEADING strip, which waits for nobody, by 15-17 % (its
+// stores share HBM with those polls).  Sleeping 64 x 64 clocks between polls:
+// feed waits per strip 3.7k -> 0.7k, leader 29.1 -> 24.6 ms, the band alone
+// 30.6 -> 28.4 ms and 2 chained bands 31.3-33.3 -> 30.1-31.0 ms at a hop of 12.3
+// instead of 11.5 us (profiles/r05y_poll_sleep.txt).  The vertical sweeps and
+// the SW fill, whose chains are latency-bound, lose with it and keep 1.
+constexpr int kPollSleepTr = 64;
+
 // Where a compute wave's feed comes from.
 enum FeedSrc { FEED_BOUNDARY = 0, FEED_GRAN = 1, FEED_LDS = 2 };
 
@@ -293,6 +304,7 @@ struct Feed {
     bool trace_pub;      // debug trace: stamp the publish of chunk 0 in this iteration
     uint64_t tpub;
     uint64_t tmo;        // watchdog bound (FillArgs::timeout_ticks)
+    bool sparse;         // poll with kPollSleepTr (horizontal strips)
 };
 
 // Where a compute wave's right column goes.
@@ -374,7 +386,8 @@ __device__ __forceinline__ void run_iter(char *__restrict__ lds, int it, const u
             if (F.ready <= c) {
                 const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
                 if (F.src == FEED_GRAN) {
-                    const uint64_t v = wait_chunk<G>(F.g, F.tag, c, ctrl, 2, F.tmo);
+                    const uint64_t v = F.sparse ? wait_chunk<G, kPollSleepTr>(F.g, F.tag, c, ctrl, 2, F.tmo)
+                                                : wait_chunk<G, 1>(F.g, F.tag, c, ctrl, 2, F.tmo);
                     F.dead |= !__all(lane / G != c || (uint32_t)(v >> 32) == F.tag);
                     if (lane / G == c) F.ring[((it & 3) << 6) + lane] = (int32_t)(uint32_t)v;
                 } else {
@@ -548,7 +561,7 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
     for (int k = 0; k < C; ++k) top[k] = (int32_t)((cl + k) * (int64_t)gt);  // SW: row 0 is 0
     if (B.halo_in != nullptr) {
         const uint64_t h0 = __builtin_amdgcn_s_memrealtime();
-        for (;;) {
+        for (uint32_t n = 1;; ++n) {
             bool ok = true;
 #pragma unroll
             for (int k = 0; k < C; ++k) {
@@ -562,11 +575,13 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
             bnd0 = (int32_t)(uint32_t)g0;
             ok &= (uint32_t)(g0 >> 32) == A.halo_tag;
             if (__all(ok)) break;
-            if (ctrl_load(A.ctrl + 1) != 0u) { dead = true; break; }
-            if (__builtin_amdgcn_s_memrealtime() - h0 > A.timeout_ticks) {
-                give_up(A.ctrl, 2u, 4, B.halo_in, A.halo_tag, 0);
-                dead = true;
-                break;
+            if (n % kPollCheck == 0u) {  // (the error word: not a hot line, nw_dev.h wait_chunk)
+                if (ctrl_load(A.ctrl + 1) != 0u) { dead = true; break; }
+                if (__builtin_amdgcn_s_memrealtime() - h0 > A.timeout_ticks) {
+                    give_up(A.ctrl, 2u, 4, B.halo_in, A.halo_tag, 0);
+                    dead = true;
+                    break;
+                }
             }
             __builtin_amdgcn_s_sleep(4);
         }
@@ -629,7 +644,14 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
     const bool fed = p == A.strip0 && A.feed_in != nullptr;
     Feed F;
     // (with a feeder wave, wave 0's granules arrive through LDS like the later waves' feeds)
-    F.src = j > 0 ? FEED_LDS : (p > 0 || fed) ? (L::kFeeder ? FEED_LDS : FEED_GRAN) : FEED_BOUNDARY;
+    // (debug probe NW_FLAG_DEBUG_NO_CHAIN: every strip unchained -- boundary feed, no publish)
+    const bool nochain = (A.flags & NW_FLAG_DEBUG_NO_CHAIN) != 0;
+    if (nochain && (A.flags & NW_FLAG_DEBUG_STAGGER)) {  // (probe: the chained sweep's start diagonal)
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        const uint64_t d = (uint64_t)(p - A.strip0) * 1150u;  // 11.5 us per strip (100 MHz ticks)
+        while (__builtin_amdgcn_s_memrealtime() - t0 < d) __builtin_amdgcn_s_sleep(8);
+    }
+    F.src = j > 0 ? FEED_LDS : ((p > 0 || fed) && !nochain) ? (L::kFeeder ? FEED_LDS : FEED_GRAN) : FEED_BOUNDARY;
     F.ring = (int32_t *)(lds + L::kFeed) + j * kFeedRows;
     F.pub = (const int32_t *)(lds + L::kCtl) + (j > 0 ? (j - 1) * L::kCtlWords + 1 : L::kFeeder ? L::kFeedWord : 1);
     const bool feeds = p == A.strip0 + A.nstrips - 1 && A.feed_out != nullptr;
@@ -642,9 +664,10 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
     F.trace_pub = false;
     F.tpub = 0;
     F.tmo = A.timeout_ticks;
+    F.sparse = A.tr != 0;
     Out O;
-    O.off = A.tr != 0 && feeds && A.tr_store_pub != 0 && (A.flags & 1) == 0;
     O.lds = j + 1 < NC;
+    O.off = (A.tr != 0 && feeds && A.tr_store_pub != 0 && (A.flags & 1) == 0) || (nochain && !O.lds);
     O.ring = (int32_t *)(lds + L::kFeed) + (j + 1 < NC ? j + 1 : j) * kFeedRows;
     O.pub = ctr + 1;
     O.gap = gap;
@@ -731,7 +754,8 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
                 if (F.ready == 0) {  // chunk 0 is needed right away
                     const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
                     if (traced) twait = w0;
-                    gv = wait_chunk<G>(F.g, F.tag, 0, A.ctrl, 6, A.timeout_ticks);
+                    gv = F.sparse ? wait_chunk<G, kPollSleepTr>(F.g, F.tag, 0, A.ctrl, 6, A.timeout_ticks)
+                                  : wait_chunk<G, 1>(F.g, F.tag, 0, A.ctrl, 6, A.timeout_ticks);
                     F.dead |= !__all(lane >= G || (uint32_t)(gv >> 32) == F.tag);
                     F.nslow += 1;
                     F.wticks += __builtin_amdgcn_s_memrealtime() - w0;

@@ -272,6 +272,8 @@ def _seq(s) -> np.ndarray:
 
 FLAG_TIMING_ONLY, FLAG_NO_PROFILE, FLAG_NO_FINISH = 1, 2, 4  # nw_params.flags (include/nw_hip.h)
 FLAG_DEBUG_DRAIN, FLAG_DEBUG_NO_STORE = 0x100, 0x200  # compute-pace probes, with FLAG_TIMING_ONLY only
+FLAG_DEBUG_NO_CHAIN = 0x400  # store-pattern probe: strips unchained, HBM stores kept, no fill
+FLAG_DEBUG_STAGGER = 0x800   # with NO_CHAIN: strip p starts p * 11.5 us after its claim
 
 
 def fill(s1, s2, scheme=(1, 0, -1), waves: int = 0, device: int = -1, substrips: int = 0,

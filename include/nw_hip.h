@@ -57,7 +57,14 @@ enum {
     /* debug probes of the compute pace: only together with NW_FLAG_TIMING_ONLY
        (refused otherwise -- the table is not written) */
     NW_FLAG_DEBUG_DRAIN = 0x100,    /* store waves drain the LDS ring without reading it */
-    NW_FLAG_DEBUG_NO_STORE = 0x200  /* no store waves at all */
+    NW_FLAG_DEBUG_NO_STORE = 0x200, /* no store waves at all */
+    /* store-pattern probe (strip kernel, no halo / feed): every strip takes the
+       boundary column instead of its left neighbour's and publishes nothing, so the
+       strips run unchained; the table IS written to HBM but holds no fill */
+    NW_FLAG_DEBUG_NO_CHAIN = 0x400,
+    /* with NO_CHAIN: strip p of a one-pass launch starts p * 11.5 us after it is
+       claimed -- the chained sweep's diagonal, without its hand-offs */
+    NW_FLAG_DEBUG_STAGGER = 0x800
 };
 
 /* nw_params.kernel: which gfx950 kernel family fills the table.  Both compute

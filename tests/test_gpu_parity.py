@@ -189,7 +189,8 @@ def test_score_range_refused():
     assert nwhip.score(small, small, (4095, -4095, -4095)) == oracle.score(small, small, (4095, -4095, -4095))
 
 
-@pytest.mark.parametrize("flags", [nwhip.FLAG_DEBUG_NO_STORE, nwhip.FLAG_DEBUG_DRAIN, 1 << 20, 8])
+@pytest.mark.parametrize("flags", [nwhip.FLAG_DEBUG_NO_STORE, nwhip.FLAG_DEBUG_DRAIN, nwhip.FLAG_DEBUG_STAGGER,
+                                   1 << 20, 8])
 def test_unknown_or_debug_flags_refused(flags):
     """Flag bits are checked: unknown bits, and the compute-pace probes (which leave
     the table unwritten) without NW_FLAG_TIMING_ONLY, are refused (NW_ERR_ARG).
@@ -198,6 +199,21 @@ def test_unknown_or_debug_flags_refused(flags):
     with pytest.raises(nwhip.NwError) as e:
         nwhip.fill(s, s, (1, 0, -1), flags=flags)
     assert e.value.status == nwhip.NW_ERR_ARG
+
+
+@pytest.mark.gpu
+def test_no_chain_probe_refused_on_bands(torch, ctx):
+    """The store-pattern probe (NW_FLAG_DEBUG_NO_CHAIN: strips unchained, no fill) is
+    refused wherever a band would hand its rows on, and accepted on a whole table."""
+    n1, rows = 1000, 100
+    d1 = torch.from_numpy(nwhip.synth(1, n1)).cuda()
+    d2 = torch.from_numpy(nwhip.synth(2, rows)).cuda()
+    tab = nwhip.Context.alloc_table(n1, rows)
+    halo = torch.zeros(n1 + 1, dtype=torch.int64, device="cuda")
+    with pytest.raises(nwhip.NwError) as e:
+        ctx.fill_band(d1, d2, tab, halo_in=halo, tag=1, row0=5000, flags=nwhip.FLAG_DEBUG_NO_CHAIN)
+    assert e.value.status == nwhip.NW_ERR_ARG
+    ctx.fill(d1, d2, tab, flags=nwhip.FLAG_DEBUG_NO_CHAIN | nwhip.FLAG_DEBUG_STAGGER, kernel=nwhip.KERNEL_STRIPS)
 
 
 def test_band_score_range_refused(torch, ctx):
