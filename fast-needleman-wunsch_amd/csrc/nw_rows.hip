@@ -527,6 +527,8 @@ __device__ __forceinline__ void feeder_in(const FillArgs &A, char *__restrict__ 
                     break;
                 }
             }
+            // (1: sparser polls change nothing here -- the leading panel is store-bound,
+            // profiles/r05zc_panel_poll_sleep.txt)
             __builtin_amdgcn_s_sleep(1);
         }
     }
