@@ -257,3 +257,26 @@ def test_sw_half_word_shape_is_sw_only(torch, ctx):
     with pytest.raises(nwhip.NwError) as e:
         ctx.fill(s, s, tab, (1, 0, -1), substrips=2, strip_waves=4)
     assert e.value.status == nwhip.NW_ERR_UNSUPPORTED
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("strip", [(2, 2), (2, 4)])
+@pytest.mark.parametrize("n1,n2", [(660, 657), (1537, 300), (5, 9)])
+def test_sw_strip_origin_column0(torch, ctx, strip, n1, n2):
+    """A 256-byte aligned table base sweeps column 0 with the strips (origin 0), also
+    for the half-word rings and their corner fix-up (match 100: cells reach 2^16 where
+    the sequences agree; the corner's strip words are indexed from origin 0)."""
+    scheme = (100, -100, -1)
+    rng = np.random.default_rng(n1 + 3 * n2)
+    s1 = rng.integers(1, 5, n1).astype(np.int8)
+    s2 = s1[:n2].copy() if n2 <= n1 else rng.integers(1, 5, n2).astype(np.int8)
+    d1, d2 = torch.from_numpy(s1).cuda(), torch.from_numpy(s2).cuda()
+    rows, pitch = nwhip.table_rows(n2), nwhip.table_pitch(n1)
+    flat = torch.empty(rows * pitch + 64, dtype=torch.int32, device="cuda")
+    shift = (-(flat.data_ptr() // 4)) % 64
+    tab = flat[shift:shift + rows * pitch].view(rows, pitch)
+    tab.fill_(-0x5A5A5A5)
+    want = oracle.sw_fill(s1, s2, scheme)
+    r = ctx.fill(d1, d2, tab, scheme, substrips=strip[0], strip_waves=strip[1], mode=nwhip.MODE_SW)
+    np.testing.assert_array_equal(tab[:n2 + 1, :n1 + 1].cpu().numpy(), want)
+    assert (r.score, r.end_i, r.end_j) == oracle.sw_best(s1, s2, scheme)
