@@ -280,3 +280,25 @@ def test_sw_strip_origin_column0(torch, ctx, strip, n1, n2):
     r = ctx.fill(d1, d2, tab, scheme, substrips=strip[0], strip_waves=strip[1], mode=nwhip.MODE_SW)
     np.testing.assert_array_equal(tab[:n2 + 1, :n1 + 1].cpu().numpy(), want)
     assert (r.score, r.end_i, r.end_j) == oracle.sw_best(s1, s2, scheme)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scheme", [(2, -1, 0), (-1, 3, -2), (0, -1, -1), (7, -5, -3)])
+@pytest.mark.parametrize("n1,n2", [(1100, 700), (513, 1024)])
+def test_sw_half_word_schemes(torch, ctx, scheme, n1, n2):
+    """(2, 4) half-word rings under gap 0, a mismatch above the match (the corner bound
+    uses max(match, mismatch)), no positive score at all, and a wide scheme: tables,
+    best cell and path equal the oracle's (all corners empty at these sizes)."""
+    rng = np.random.default_rng(n1 + n2 + sum(scheme))
+    s1 = rng.integers(1, 5, n1).astype(np.int8)
+    s2 = rng.integers(1, 5, n2).astype(np.int8)
+    d1, d2 = torch.from_numpy(s1).cuda(), torch.from_numpy(s2).cuda()
+    tab = nwhip.Context.alloc_table(n1, n2)
+    tab.fill_(-0x5A5A5A5)
+    r = ctx.fill(d1, d2, tab, scheme, substrips=2, strip_waves=4, mode=nwhip.MODE_SW)
+    want = oracle.sw_fill(s1, s2, scheme)
+    np.testing.assert_array_equal(tab[:n2 + 1, :n1 + 1].cpu().numpy(), want)
+    assert (r.score, r.end_i, r.end_j) == oracle.sw_best(s1, s2, scheme)
+    al, ops = ctx.sw_traceback(d1, d2, tab, (r.end_i, r.end_j), scheme)
+    wops, bi, bj = oracle.sw_traceback(s1, s2, want, (r.end_i, r.end_j), scheme)
+    np.testing.assert_array_equal(ops, wops)
