@@ -348,13 +348,70 @@ def run_sw(args):
     print(json.dumps(out), flush=True)
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_plan(gpus: int, world_env: str | None, ndev: int, share_gpu: bool) -> tuple[str, str]:
+    """How bench.py runs for --gpus `gpus` (the program owns its rank setup, as
+    mpi-horz-driver.cpp:14-32 does): ("single", ""), ("ranks", "") when a launcher
+    already started one process per rank, ("spawn", "") when this process must start
+    `gpus` ranks itself, or ("refuse", why).  Pure: ndev = torch.cuda.device_count()
+    (which initialises no GPU on this image), world_env = $WORLD_SIZE or None."""
+    if gpus < 1:
+        return "refuse", f"--gpus {gpus}: need at least 1"
+    if world_env not in (None, ""):
+        try:
+            world = int(world_env)
+        except ValueError:
+            return "refuse", f"WORLD_SIZE={world_env!r} is not an integer"
+        if world != gpus:
+            return "refuse", (f"WORLD_SIZE={world} but --gpus {gpus}: the launcher started a different number "
+                              "of ranks than the line would report")
+        if world == 1:
+            return "single", ""
+        if not share_gpu and ndev < world:
+            return "refuse", (f"{world} ranks but {ndev} visible GPU(s): one rank per GPU needs {world} "
+                              "(--share-gpu rehearses all ranks on device 0)")
+        return "ranks", ""
+    if gpus == 1:
+        return "single", ""
+    if ndev < 1:
+        return "refuse", "no visible GPU"
+    if not share_gpu and ndev < gpus:
+        return "refuse", (f"--gpus {gpus} but {ndev} visible GPU(s) (--share-gpu rehearses all ranks on "
+                          "device 0)")
+    return "spawn", ""
+
+
+def spawn_ranks(gpus: int) -> int:
+    """`python bench.py --gpus N` with no launcher: start N ranks under
+    torch.distributed.run as a CHILD process (never an exec: this process has made no
+    GPU call, and the ranks make their own), with the rendezvous on 127.0.0.1.  The
+    ranks inherit stdout, so rank 0's JSON line is this command's line.  Returns the
+    child's exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, NW_BENCH_LAUNCHER="self")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     args = parse()
     if args.workload == "sw":
         run_sw(args)
         return
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if args.gpus > 1 or world > 1:
+    import torch
+    plan, why = launch_plan(args.gpus, os.environ.get("WORLD_SIZE"), torch.cuda.device_count(), args.share_gpu)
+    if plan == "refuse":
+        print(f"bench.py: refusing to run: {why}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if plan == "spawn":
+        sys.exit(spawn_ranks(args.gpus))
+    if plan == "ranks":
         import nw_bands  # multi-GPU row bands (+ column bands as the alternate leg)
         nw_bands.cpu_baseline_fn = cpu_baseline
         nw_bands.run_bands(args)

@@ -372,6 +372,8 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
     if (!valid_params(p)) return NW_ERR_ARG;
     const bool sw = p->mode == NW_MODE_SW;
     if (sw && (band || cb)) return NW_ERR_UNSUPPORTED;  // (local alignment: single table, config 5)
+    // the unchained probe leaves no valid table, so no best cell / locate either
+    if (sw && (p->flags & NW_FLAG_DEBUG_NO_CHAIN)) return NW_ERR_ARG;
     if ((p->flags & NW_FLAG_DEBUG_NO_CHAIN) && (band || cb)) return NW_ERR_ARG;  // (no fill to hand on)
     if (band && cb) return NW_ERR_ARG;
     // The kernels hold w = t - GAP*(i+j) in int32 next to a "minus infinity" of
@@ -555,7 +557,9 @@ static int launch_fill(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *
         if (!c->swinfo) NW_HIP_TRY(hipMalloc(&c->swinfo, 16 * sizeof(int64_t)));  // [0..9] traceback info, [12] locate key
         int32_t *best = c->smax + s.nstrips;
         uint64_t *key = (uint64_t *)(c->swinfo + 12);
-        if (half && nw::launch_sw_fixup(d_t, pitch, n1, n2, (const uint8_t *)d_s1, (const uint8_t *)d_s2, p->match,
+        // (TIMING_ONLY: the strips stored into a scratch tile and the caller's table
+        // was never written, so there is no corner to fix up in it)
+        if (half && !(p->flags & NW_FLAG_TIMING_ONLY) && nw::launch_sw_fixup(d_t, pitch, n1, n2, (const uint8_t *)d_s1, (const uint8_t *)d_s2, p->match,
                                         p->mismatch, p->gap, col0, (int32_t)(nw::kWave * s.K * s.NC), c->smax,
                                         stream) != hipSuccess)
             return NW_ERR_HIP;

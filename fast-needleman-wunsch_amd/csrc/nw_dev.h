@@ -80,10 +80,11 @@ __device__ __forceinline__ void ctr_store(int32_t *p, int32_t v) {
 // same box, profiles/r04c_poll_ab.txt: 256k panels 44.9 -> 48.7 ms, SW 64k strip
 // fill 6.3 -> 7.5 ms: the extra loads of every waiting wave compete with the
 // fill's own traffic.)  The error word and the watchdog are checked every
-// kPollCheck polls only: every waiting wave of the chip re-reading the one error
-// word after each poll made it a hot line and doubled each poll's round trip
-// (round 5: profiles/r05w_poll_split.txt).  The loads are global (the generic
-// pointer of a noinline callee would make them flat loads).
+// kPollCheck polls only, so a poll is one round trip instead of two and the one
+// error word is not re-read by every waiting wave of the chip after each poll
+// (round 5, measured neutral on the band, the SW fill and the 256k bench: the
+// r05x section of profiles/r05y_poll_sleep.txt).  The loads are global (the
+// generic pointer of a noinline callee would make them flat loads).
 constexpr uint32_t kPollCheck = 32;
 template <int G, int SLEEP>
 __device__ __noinline__ uint64_t wait_chunk(const uint64_t *g, uint32_t tag, int c,

@@ -9,9 +9,11 @@
 //   t[0][j] = j*GAP, t[i][0] = i*GAP                              (serial.cpp:16-17)
 //
 // Decomposition (DESIGN.md section 4 has the full picture):
-//   * Columns col0 .. n1 are cut into vertical STRIPS of NC*64*C columns (by
-//     default NC = 2 chained compute waves of C = 2 columns per lane: 256
-//     columns, one strip per CU at a time).  col0 = 1 when the table base is
+//   * Columns col0 .. n1 are cut into vertical STRIPS of NC*64*C columns (NC
+//     chained compute waves of C columns per lane; the tuned shapes are the
+//     256-column (4,1), (2,2) and (1,4), csrc/nw_tuned.h -- (2,2) for the SW
+//     fill, (4,1) for every row band -- while whole tables as wide as config 3
+//     go to the panel kernel, nw_rows.hip; one strip per CU at a time).  col0 = 1 when the table base is
 //     laid out so that column 1 starts a 256-byte line (nw_table_offset): then
 //     the boundary column 0 (t[i][0] = i*GAP) is not swept at all and an
 //     N x N table is exactly N/256 strips.  Each strip is swept top to bottom
@@ -46,8 +48,8 @@
 //   * Each compute wave reads its right column (lane 63, column C-1) back from
 //     its ring 16 rows at a time and publishes it: into the next compute
 //     wave's LDS feed ring (+ a counter), or -- for the strip's last wave -- as
-//     8-byte {tag, value} granules in HBM (agent-scope atomic stores; the data
-//     is the flag) for the next strip's first wave, which polls them -- the
+//     8-byte {tag, value} granules in HBM (system-scope atomic stores, nw_dev.h
+//     NW_GRAN_SCOPE; the data is the flag) for the next strip's first wave, which polls them -- the
 //     GPU analogue of idxarray-mt's per-row progress counters
 //     (idxarray-mt.cpp:8,44,50-56).
 //   * Strips are claimed from an atomic ticket in increasing order by a
@@ -105,9 +107,12 @@ struct Lay {
     static constexpr int kRing = kR * kSlot;          // ring bytes (a power of two)
     static constexpr int kFeed = NC * kRing;          // byte offset of the feed rings
     static constexpr int kCtl = kFeed + NC * kFeedRows * 4;
-    // counters, 8 words per compute wave j: [0] steps written, [1] rows of its
-    // right column published into wave j+1's feed, [2] iterations done,
-    // [3 + q] rows read by its store wave q; then the strip word
+    // counters, kCtlWords words per compute wave j: [0] steps written, [1] rows of
+    // its right column published into wave j+1's feed, [2] iterations done,
+    // [3 + q] rows read by its store wave q; then the strip word.  3 + kSPR <= 8
+    // are used (the static_assert below); the block is 16 words (64 bytes) since
+    // round 5's five store waves, which is padding: 8 would also hold them, but the
+    // LDS layout of the measured build is kept as it is
     static constexpr int kCtlWords = 16;
     static constexpr int kStripWord = NC * kCtlWords;
     static constexpr int kBytes = kCtl + (kStripWord + 4) * 4;
@@ -125,11 +130,14 @@ struct Lay {
     static constexpr int kBatch = C == 4 ? 8 : 16;
     // FEEDER wave (opt-in build NW_FEEDER; one per workgroup, the last): polls the
     // left strip's granules and fills compute wave 0's feed ring + counter (ctl word
-    // kFeedWord), so that wave 0 waits on LDS only.  Measured (profiles/
-    // r04g_feeder_ab.txt): hop 11.7 -> 8.5 us on the horizontal band, but the band
-    // 32.7 -> 42.1 ms and the SW fill 6.6 -> 7.0 ms: the compute waves then spend
-    // 10 % more cycles per step inside run_iter (profiles/r04s_feeder_cycles.txt), so
-    // it stays off.  Not for shapes whose workgroup would then exceed 8 waves
+    // kFeedWord), so that wave 0 waits on LDS only (it then takes the FEED_LDS path:
+    // no granule loads in its prefetch pipeline).  Measured (profiles/
+    // r04g_feeder_ab.txt, r05g_feeder_trace.txt, r05zi_feeder_revisited.txt): hop
+    // 11.7 -> 7.2-8.5 us on the horizontal band, but the band 32.7 -> 39-42 ms and
+    // the SW fill 6.6 -> 7.0 ms: the fed compute waves wait on their feeder at nearly
+    // every 16-row chunk (26-28k waits per strip against 5k) and sporadic long hops
+    // propagate down the chain ("The feeder question"), so it
+    // stays off.  Not for shapes whose workgroup would then exceed 8 waves
     // (register budget).
 #ifdef NW_FEEDER
     static constexpr bool kFeeder = NC * (1 + kSPR) < 8;

@@ -599,6 +599,28 @@ def gather_fill_latencies(stamps, world: int) -> dict:
     return fill_latencies(allst)
 
 
+CLOCK = "CLOCK_MONOTONIC (time.monotonic_ns), every rank on one host"
+
+
+def same_host(hosts) -> bool:
+    """True when every rank reported the same host name (fill_latencies compares
+    CLOCK_MONOTONIC stamps across ranks, which is meaningful on one host only; the
+    reference's epoch milliseconds, mpi-horz-driver.cpp:39-50, would need synchronised
+    node clocks instead -- multi-node runs are out of scope)."""
+    return len(set(hosts)) <= 1
+
+
+def check_one_host(world: int) -> None:
+    """All-gather the host names and refuse a multi-host world (see same_host)."""
+    import socket
+    import torch.distributed as dist
+    hosts = [None] * world
+    dist.all_gather_object(hosts, socket.gethostname())
+    if not same_host(hosts):
+        raise RuntimeError(f"ranks span several hosts {sorted(set(hosts))}: the per-fill timing compares "
+                           "CLOCK_MONOTONIC stamps across ranks and is single-node only")
+
+
 PING = 0x5A5A0000  # pre-flight marker (never a launch tag: tags count launches from 1)
 
 
@@ -747,9 +769,13 @@ def run_bands(args) -> dict | None:
 
     rank, world = _env_int("RANK", 0), _env_int("WORLD_SIZE", 1)
     local = _env_int("LOCAL_RANK", rank)
+    if world != args.gpus:
+        raise RuntimeError(f"run_bands: WORLD_SIZE={world} but --gpus {args.gpus} (bench.py refuses this)")
     ndev = torch.cuda.device_count()
     if ndev == 0:
         raise RuntimeError("run_bands needs a GPU (there is no CPU fallback)")
+    if not args.share_gpu and ndev < world:
+        raise RuntimeError(f"run_bands: {world} ranks but {ndev} visible GPU(s) and no --share-gpu")
     dev = 0 if args.share_gpu else local % ndev
     torch.cuda.set_device(dev)
     if not dist.is_initialized():
@@ -757,6 +783,7 @@ def run_bands(args) -> dict | None:
         # failing within minutes rather than gloo's default half hour
         import datetime
         dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=300))
+    check_one_host(world)
     scheme = tuple(int(x) for x in args.scheme.split(","))
     legs = {}
     plan_ = legs_for(args)
@@ -800,7 +827,7 @@ cpu_baseline_fn = None  # bench.py installs its cpu_baseline (rank 0 only report
 def band_traffic(n1: int, rows: int, sweep: str):
     """HBM bytes per launch of one GPU's row-band kernel (WRITE_SIZE + 2 x FETCH_SIZE)
     from the committed rocprofv3 PMC record of that band filled alone on one GPU
-    (profiles/pmc_traffic.json, tools/r04/profile.sh: config 4's last band, 65538 x
+    (profiles/pmc_traffic.json, tools/profile_lease.sh: config 4's last band, 65538 x
     524289), and where it came from; (None, None) for a geometry without a record."""
     path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
                         "pmc_traffic.json")
@@ -876,12 +903,15 @@ def _line(args, world: int, scheme, part: str, ms: list) -> dict:
         "value": round(value, 2),
         "unit": "GCUPS",
         "n_gpus": world,
+        "requested_gpus": args.gpus,
+        "launcher": os.environ.get("NW_BENCH_LAUNCHER", "external"),
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_step, 3),
         "timing": "per fill: each timed fill alone (barrier + synchronize around it), earliest rank start -> "
                   "latest rank end on the host's CLOCK_MONOTONIC (mpi-horz-driver.cpp:38-83); value = cells / "
                   "mean per-fill time",
+        "clock": CLOCK,
         "per_fill_ms": [round(x, 3) for x in fills["ms"]],
         "start_skew_ms_max": round(max(fills["start_skew_ms"]), 3),
         "timed_region_ms_per_step": round(wall_s / args.steps * 1e3, 3),

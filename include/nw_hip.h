@@ -60,7 +60,8 @@ enum {
     NW_FLAG_DEBUG_NO_STORE = 0x200, /* no store waves at all */
     /* store-pattern probe (strip kernel, no halo / feed): every strip takes the
        boundary column instead of its left neighbour's and publishes nothing, so the
-       strips run unchained; the table IS written to HBM but holds no fill */
+       strips run unchained; the table IS written to HBM but holds no fill (refused
+       on bands and in NW_MODE_SW, whose best cell would be meaningless) */
     NW_FLAG_DEBUG_NO_CHAIN = 0x400,
     /* with NO_CHAIN: strip p of a one-pass launch starts p * 11.5 us after it is
        claimed -- the chained sweep's diagonal, without its hand-offs */

@@ -214,6 +214,12 @@ def test_no_chain_probe_refused_on_bands(torch, ctx):
         ctx.fill_band(d1, d2, tab, halo_in=halo, tag=1, row0=5000, flags=nwhip.FLAG_DEBUG_NO_CHAIN)
     assert e.value.status == nwhip.NW_ERR_ARG
     ctx.fill(d1, d2, tab, flags=nwhip.FLAG_DEBUG_NO_CHAIN | nwhip.FLAG_DEBUG_STAGGER, kernel=nwhip.KERNEL_STRIPS)
+    #  Smith-Waterman: an unchained table has no meaningful best cell
+    for fl in (nwhip.FLAG_DEBUG_NO_CHAIN, nwhip.FLAG_DEBUG_NO_CHAIN | nwhip.FLAG_TIMING_ONLY):
+        with pytest.raises(nwhip.NwError) as e:
+            ctx.fill(d1, d2, tab, scheme=(1, -1, -1), mode=nwhip.MODE_SW, flags=fl, kernel=nwhip.KERNEL_STRIPS)
+        assert e.value.status == nwhip.NW_ERR_ARG
+    torch.cuda.synchronize()
 
 
 def test_band_score_range_refused(torch, ctx):

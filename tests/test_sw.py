@@ -249,6 +249,22 @@ def test_sw_half_word_corner(torch, ctx, n, mutate):
 
 
 @pytest.mark.gpu
+def test_sw_half_word_timing_only_leaves_table_alone(torch, ctx):
+    """ NW_FLAG_TIMING_ONLY on the (2, 4) half-word path: the strips store
+    into a scratch tile, so the corner fix-up must not run on the caller's (unwritten)
+    table either -- every byte of it stays as it was, corner included."""
+    scheme = (100, -100, -1)
+    n = 660
+    s1, s2 = _half_word_pair(n, 0.0, n)
+    d1, d2 = torch.from_numpy(s1).cuda(), torch.from_numpy(s2).cuda()
+    tab = nwhip.Context.alloc_table(n, n)
+    tab.fill_(-0x5A5A5A5)
+    ctx.fill(d1, d2, tab, scheme, substrips=2, strip_waves=4, mode=nwhip.MODE_SW, flags=nwhip.FLAG_TIMING_ONLY)
+    torch.cuda.synchronize()
+    assert bool((tab == -0x5A5A5A5).all())
+
+
+@pytest.mark.gpu
 def test_sw_half_word_shape_is_sw_only(torch, ctx):
     """The half-word rings hold Smith-Waterman cells only: an NW fill with (2, 4) is
     refused rather than wrapped."""

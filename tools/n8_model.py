@@ -16,7 +16,7 @@ neighbour).  The durations are those of the band alone: contention between the
 bands of one node is per GPU (each has its own HBM), so only the shift of a band's
 strip starts changes what each strip meets, which the model ignores.
 
-  python tools/n8_model.py profiles/r04e_vband_w256.npz [--bands 8] [--n1-ms 44.9]
+  python tools/n8_model.py profiles/r04m_vband_def_w256.npz [--bands 8] [--n1-ms 44.9]
 prints the modelled N-band step time, GCUPS and the ratio to the N = 1 bench.
 """
 import argparse

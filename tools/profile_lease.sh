@@ -6,7 +6,7 @@
 #   band_{v,h}_{kt,w,f}/  the same three passes over one config-4 rank's band filled alone
 #                         (tools/band_alone.py --rank 7, vertical / horizontal sweep)
 # then: python tools/summarize_r04.py <outdir> <tag>
-# Usage: bash tools/r04/profile.sh <outdir>
+# Usage: bash tools/profile_lease.sh <outdir>
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/$1

@@ -1,4 +1,4 @@
-"""Summarise a tools/r04/profile.sh output directory into profiles/ (round 4 onwards).
+"""Summarise a tools/profile_lease.sh output directory into profiles/ (round 4 onwards).
 
 Each profiled program ran three times under rocprofv3 (MI355X_MICROARCH.md HBM /
 rocprofv3 recipe: a kernel-trace --stats pass and one --pmc pass per counter):
