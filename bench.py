@@ -68,6 +68,9 @@ def parse():
                          "the single-table fill (band r+1 waits for band r's strips to reach its last "
                          "row); auto = horizontal (the shorter chain at N = 8, DESIGN.md section 5); "
                          "the other runs as an alternate leg")
+    ap.add_argument("--tband-shape", default=None,
+                    help="N>1 horizontal-strip row bands: strip shape 'C,NC', 4,1 or 2,2 (default: "
+                         "nw_bands.TBAND_SHAPE)")
     ap.add_argument("--kernel", type=int, default=0,
                     help="0 auto, 1 anti-diagonal strips, 2 row-scan panels (nw_params.kernel)")
     ap.add_argument("--col-width", type=int, default=65536,

@@ -658,9 +658,14 @@ int nw_fill_tband_async(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t 
         tb->row0 < 0 || tb->row0 + R >= INT32_MAX)
         return NW_ERR_ARG;
     if (!valid_params(p)) return NW_ERR_ARG;
-    if (p->mode != NW_MODE_NW || p->kernel == NW_KERNEL_PANELS || (p->substrips != 0 && p->substrips != 4) ||
-        (p->strip_waves != 0 && p->strip_waves != 1))
-        return NW_ERR_UNSUPPORTED;
+    // shapes: (4, 1) (the default) or (2, 2) -- 256-row strips either way
+    if (p->mode != NW_MODE_NW || p->kernel == NW_KERNEL_PANELS) return NW_ERR_UNSUPPORTED;
+    int tC = 4, tNC = 1;
+    if (p->substrips != 0 || p->strip_waves != 0) {
+        tC = p->substrips ? p->substrips : 4;
+        tNC = p->strip_waves ? p->strip_waves : 1;
+        if (!((tC == 4 && tNC == 1) || (tC == 2 && tNC == 2))) return NW_ERR_UNSUPPORTED;
+    }
     if (tb->tag == 0 || (((uintptr_t)tb->feed_in | (uintptr_t)tb->feed_out) & 7u) != 0) return NW_ERR_ARG;
     if ((tb->row0 > 0) != (tb->feed_in != nullptr)) return NW_ERR_ARG;
     if (tb->feed_out && (p->flags & 1)) return NW_ERR_ARG;  // needs the real last row
@@ -673,7 +678,7 @@ int nw_fill_tband_async(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t 
     NW_HIP_TRY(hipSetDevice(c->device));
     // the transposed band: R + 1 "columns" (global rows row0 .. row0 + R, the first
     // one the feed), n1 + 1 "rows" (the band's columns)
-    Shape s = make_shape(R, n1, p->waves, 4, 1, c->cus, 1, false, NW_KERNEL_STRIPS);
+    Shape s = make_shape(R, n1, p->waves, tC, tNC, c->cus, 1, false, NW_KERNEL_STRIPS);
     if (!shape_valid(s) || s.nstrips > INT32_MAX / 2 || s.nblocks > INT32_MAX / 2) return NW_ERR_ARG;
     // Leftover rows: when the band's last strip would run ALONE as one more pass over
     // all n1 columns (strips = k * workers + 1, e.g. config 4's last band: 65537 rows =
@@ -684,7 +689,7 @@ int nw_fill_tband_async(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t 
         !(p->flags & 1)) {
         L = R - 256 * (s.nstrips - 1);
         Rs = R - L;
-        s = make_shape(Rs, n1, p->waves, 4, 1, c->cus, 1, false, NW_KERNEL_STRIPS);
+        s = make_shape(Rs, n1, p->waves, tC, tNC, c->cus, 1, false, NW_KERNEL_STRIPS);
         if (!shape_valid(s)) return NW_ERR_ARG;
     }
     int st;
@@ -755,9 +760,9 @@ int nw_fill_tband_async(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t 
             const char *e = std::getenv("NW_TR_PUB_COMPUTE");
             return e != nullptr && e[0] == '1';
         }();
-        a.tr_store_pub = compute_pub ? 0 : 1;
+        a.tr_store_pub = compute_pub && tNC == 1 ? 0 : 1;  // ((2, 2): the store waves publish)
     }
-    if (nw::launch_fill(a, 4, 1, (int)s.waves, stream) != hipSuccess) return NW_ERR_HIP;
+    if (nw::launch_fill(a, tC, tNC, (int)s.waves, stream) != hipSuccess) return NW_ERR_HIP;
     if (nw::launch_tband_edges(tb->feed_in, d_t, pitch, n1, R + 1, p->gap, tb->row0, stream) != hipSuccess)
         return NW_ERR_HIP;
     c->tagbase += (uint32_t)s.nstrips + 1u;

@@ -125,7 +125,10 @@ struct Lay {
     static constexpr bool kGrp = C == 1;
     // store waves per compute wave: 5 for C = 4 (3 until round 5, 3 / 5 / 7 measured in
     // profiles/r05l_store_waves_ab.txt)
-    static constexpr int kSPR = C == 4 ? 5 : C == 1 ? 1 : 2;  // ((2,4): 1 / 3 slower, r05t)
+#ifndef NW_SPR22
+#define NW_SPR22 2
+#endif
+    static constexpr int kSPR = C == 4 ? 5 : C == 1 ? 1 : (C == 2 && NC == 2) ? NW_SPR22 : 2;  // ((2,4): 1 / 3 slower, r05t)
     static_assert(3 + kSPR <= kCtlWords, "counter words per compute wave");
     static constexpr int kBatch = C == 4 ? 8 : 16;
     // FEEDER wave (opt-in build NW_FEEDER; one per workgroup, the last): polls the
@@ -672,10 +675,12 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
     F.trace_pub = false;
     F.tpub = 0;
     F.tmo = A.timeout_ticks;
-    F.sparse = A.tr != 0;
+    // sparse polls (kPollSleepTr) for the (4, 1) horizontal strips only: the (2, 2)
+    // ones poll with them at a 24 us hop, with s_sleep 1 at 11 us (profiles/r06c_tband22.txt)
+    F.sparse = A.tr != 0 && NC == 1;
     Out O;
     O.lds = j + 1 < NC;
-    O.off = (A.tr != 0 && feeds && A.tr_store_pub != 0 && (A.flags & 1) == 0) || (nochain && !O.lds);
+    O.off = !O.lds && ((A.tr != 0 && feeds && A.tr_store_pub != 0 && (A.flags & 1) == 0) || nochain);
     O.ring = (int32_t *)(lds + L::kFeed) + (j + 1 < NC ? j + 1 : j) * kFeedRows;
     O.pub = ctr + 1;
     O.gap = gap;
@@ -1120,31 +1125,34 @@ __device__ __forceinline__ void store_strip(const FillArgs &A, char *__restrict_
     }
 }
 
-// Store wave q of a HORIZONTAL strip (row band in horizontal strips,
-// nw_fill_tband_async; the (4, 1) shape).  The strip runs along the band's
-// rows: ring row x (step s holds rows x = s - a of compute lanes a) is table
-// COLUMN x, and compute lane a's 16-byte piece holds table rows y = c0 + 4a + k,
-// k < 4 (global numbering; local row y - tr_y0).  Columns leave in batches of 32
-// (x = 1 + 32b .. +31: 128-byte row segments, aligned when column 1 starts a
-// 256-byte line), dealt round robin to the kSPR store waves.  Store lane
-// (g, l8) = (lane / 8, lane % 8) takes, for each block of 8 compute lanes
-// a = 8 blk + l8, the 4 x 4 tile rows 4a .. 4a+3 x columns x0 + 4g .. +3 with
-// four ds_read_b128 (slot (x + a) mod kR, byte 16a: the 8 lanes the LDS serves
-// together hit 8 distinct 16-byte bank groups) and stores it as four 16-byte row
-// pieces: one store instruction = 8 rows x 128 bytes.  A wave publishes its
-// first batch start before reading anything (rows below it are none of its
-// business): with 3 waves x 32 columns the ring's slack would otherwise run out
-// before the third wave's first batch is complete.
+// Store wave q of ring j of a HORIZONTAL strip (row band in horizontal strips,
+// nw_fill_tband_async; the (4, 1) and (2, 2) shapes).  The strip runs along the
+// band's rows: ring row x (step s holds rows x = s - a of compute lanes a) is table
+// COLUMN x, and compute lane a of wave j holds table rows y = c0 + C a + k, k < C
+// (c0 = the strip's first global row + 64 C j; local row y - tr_y0).  Columns leave
+// in batches of 32 (x = 1 + 32b .. +31: 128-byte row segments, aligned when column
+// 1 starts a 256-byte line), dealt round robin to the ring's kSPR store waves.  Store
+// lane (g, l8) = (lane / 8, lane % 8) takes, for each block of 8 compute lanes
+// a = 8 blk + l8, the C x 4 tile rows C a .. C a + C-1 x columns x0 + 4g .. +3 with
+// four ds_read_b(32 C) (slot (x + a) mod kR, byte 4 C a: the 8 lanes the LDS serves
+// together hit 8 distinct pieces of one slot) and stores it as C 16-byte row pieces:
+// one store instruction = 8 rows (stride C) x 128 bytes.  A wave publishes its first
+// batch start before reading anything (rows below it are none of its business): with
+// 3 waves x 32 columns the ring's slack would otherwise run out before the third
+// wave's first batch is complete.
 template <int C, int NC>
 __device__ __forceinline__ void store_strip_tr(const FillArgs &A, char *__restrict__ lds, const Blk &B,
-                                               int q, int lane) {
-    static_assert(C == 4 && NC == 1, "horizontal strips: the (4, 1) shape");
+                                               int j, int q, int lane) {
+    static_assert((C == 4 && NC == 1) || (C == 2 && NC == 2), "horizontal strips: the (4, 1) / (2, 2) shapes");
     typedef Lay<C, NC> L;
+    typedef typename Vec<C>::T VT;
     constexpr int BATCH = 32, NS = L::kSPR, NBLK = 8;
     static_assert(BATCH + 63 + L::kChk + L::kPub <= kR, "a batch must fit the ring's slack");
     const int p = B.pk;
-    int32_t *ctr = (int32_t *)(lds + L::kCtl);
-    const int64_t c0 = A.col0 + (int64_t)p * (64 * C);  // global row of compute lane 0's first piece
+    int32_t *ctr = (int32_t *)(lds + L::kCtl) + j * L::kCtlWords;
+    const char *ring = lds + j * L::kRing;
+    // global row of ring j's compute lane 0's first piece
+    const int64_t c0 = A.col0 + (int64_t)p * (64 * C * NC) + (int64_t)j * (64 * C);
     const int32_t nx = (int32_t)(A.n2 + 1);             // ring rows = table columns 0 .. n2
     const bool timing = (A.flags & 1) != 0;
     const int g = lane >> 3, l8 = lane & 7;
@@ -1157,36 +1165,38 @@ __device__ __forceinline__ void store_strip_tr(const FillArgs &A, char *__restri
         return;
     }
     // The band's last strip publishes the band's last row (strip-local row tr_pub =
-    // 4 a* + k*: compute lane a*, piece element k*) into the next band's feed, one
-    // {tag, w} granule per column, from HERE rather than from the compute wave: the
-    // feed is fine-grained memory whose system-scope stores complete slowly, and a
-    // compute wave that issued them waits for them at each of its own prefetch
-    // waits (vmcnt counts stores too).  The 8 lanes (g, a* % 8) hold the row's 32
-    // columns of each batch (block a* / 8, element k*).  Store wave 0 also publishes
-    // column 0 (w = t - GAP*y = 0 for the boundary column t[y][0] = y*GAP) and the
-    // padding granules of the last 64-column block (tag only).
+    // 64 C j* + C a* + k*: ring j*, compute lane a*, piece element k*) into the next
+    // band's feed, one {tag, w} granule per column, from HERE rather than from the
+    // compute wave: the feed is fine-grained memory whose system-scope stores complete
+    // slowly, and a compute wave that issued them waits for them at each of its own
+    // prefetch waits (vmcnt counts stores too).  The 8 lanes (g, a* % 8) of ring j*'s
+    // store waves hold the row's 32 columns of each batch (block a* / 8, element k*).
+    // Store wave 0 of ring j* also publishes column 0 (w = t - GAP*y = 0 for the
+    // boundary column t[y][0] = y*GAP) and the padding granules of the last 64-column
+    // block (tag only).
+    const int jpub = A.tr_pub / (64 * C), lpub = A.tr_pub % (64 * C);
     const bool tpub = A.tr != 0 && A.tr_store_pub != 0 && A.feed_out != nullptr &&
-                      p == A.strip0 + A.nstrips - 1 && !timing;
-    const int pas = A.tr_pub >> 2, pks = A.tr_pub & 3;
+                      p == A.strip0 + A.nstrips - 1 && !timing && j == jpub;
+    const int pas = lpub / C, pks = lpub % C;
     const bool plane = tpub && l8 == (pas & 7);
     const uint64_t ptag = (uint64_t)A.feed_tag << 32;
     if (tpub && q == 0) {
         const int32_t x = lane == 0 ? 0 : nx - 1 + lane;
         if (x < 64 * A.nblocks) gran_store(A.feed_out + x, ptag);
     }
-    // rows of this lane: y = c0 + 4 (8 blk + l8) + k; valid while y <= n1 (the band's last row)
+    // rows of this lane: y = c0 + C (8 blk + l8) + k; valid while y <= n1 (the band's last row)
     uint32_t rmask = 0;
 #pragma unroll
     for (int blk = 0; blk < NBLK; ++blk)
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            rmask |= (c0 + 4 * (8 * blk + l8) + k <= A.n1 ? 1u : 0u) << (4 * blk + k);
+        for (int k = 0; k < C; ++k)
+            rmask |= (c0 + C * (8 * blk + l8) + k <= A.n1 ? 1u : 0u) << (C * blk + k);
     const int64_t rowb = timing ? 0 : A.pitch;  // int32 elements per table row
     int32_t *base = timing ? A.scratch + (int64_t)blockIdx.x * kScratchWords + 4 * g
-                           : B.table + (c0 - A.tr_y0 + 4 * l8) * A.pitch + 4 * g;
-    // GAP * (x + y) of element (blk, e, k) = kb + ug * (32 blk + e + k) + ug * f
-    const uint32_t kb = ug * (uint32_t)(4 * g) + ug * (uint32_t)(c0 + 4 * l8);
-    const uint32_t bpos = (uint32_t)l8 * 16u;  // byte of compute lane a = 8 blk + l8 within its slot: + 128 blk
+                           : B.table + (c0 - A.tr_y0 + C * l8) * A.pitch + 4 * g;
+    // GAP * (x + y) of element (blk, e, k) = kb + ug * (8 C blk + e + k) + ug * f
+    const uint32_t kb = ug * (uint32_t)(4 * g) + ug * (uint32_t)(c0 + C * l8);
+    const uint32_t bpos = (uint32_t)l8 * (4u * C);  // byte of compute lane a = 8 blk + l8 within its slot: + 32 C blk
     int32_t avail = 0;
     for (int32_t f = f0; f < nx; f += NS * BATCH) {
         const int32_t want = min(f + BATCH, nx);
@@ -1201,13 +1211,13 @@ __device__ __forceinline__ void store_strip_tr(const FillArgs &A, char *__restri
             ctr_store(mine, f + NS * BATCH);
             continue;
         }
-        u32x4 v[NBLK][4];
+        VT v[NBLK][4];
 #pragma unroll
         for (int blk = 0; blk < NBLK; ++blk)
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const uint32_t slot = (uint32_t)(f + 4 * g + e + 8 * blk + l8) & (uint32_t)(kR - 1);
-                v[blk][e] = *(const u32x4 *)(lds + slot * L::kSlot + bpos + 128u * blk);
+                v[blk][e] = *(const VT *)(ring + slot * L::kSlot + bpos + (32u * C) * blk);
             }
         // the batch is in registers: release its ring rows before the stores
         lds_order();
@@ -1218,7 +1228,9 @@ __device__ __forceinline__ void store_strip_tr(const FillArgs &A, char *__restri
                 uint32_t w = 0;
 #pragma unroll
                 for (int blk = 0; blk < NBLK; ++blk)
-                    if (blk == (pas >> 3)) w = pks == 0 ? v[blk][e][0] : pks == 1 ? v[blk][e][1] : pks == 2 ? v[blk][e][2] : v[blk][e][3];
+#pragma unroll
+                    for (int k = 0; k < C; ++k)
+                        if (blk == (pas >> 3) && k == pks) w = (uint32_t)comp<C>(v[blk][e], k);
                 const int32_t x = f + 4 * g + e;
                 if (x < nx) gran_store(A.feed_out + x, ptag | w);
             }
@@ -1229,12 +1241,13 @@ __device__ __forceinline__ void store_strip_tr(const FillArgs &A, char *__restri
 #pragma unroll
         for (int blk = 0; blk < NBLK; ++blk)
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < C; ++k) {
                 u32x4 o;
 #pragma unroll
-                for (int e = 0; e < 4; ++e) o[e] = v[blk][e][k] + kf + ug * (uint32_t)(32 * blk + e + k);
-                if (xok && ((rmask >> (4 * blk + k)) & 1u))
-                    *(u32x4 *)(col + (int64_t)(32 * blk + k) * rowb) = o;
+                for (int e = 0; e < 4; ++e)
+                    o[e] = (uint32_t)comp<C>(v[blk][e], k) + kf + ug * (uint32_t)(8 * C * blk + e + k);
+                if (xok && ((rmask >> (C * blk + k)) & 1u))
+                    *(u32x4 *)(col + (int64_t)(8 * C * blk + k) * rowb) = o;
             }
     }
     ctr_store(mine, kDone);
@@ -1533,11 +1546,11 @@ __global__ __launch_bounds__((64 * Lay<C, NC>::kWaves)) void nw_fill_strips(Fill
             const int b = wave - NC;
             if constexpr (L::kGrp) {
                 store_strip_grp<NC>(A, lds, B, b % NC, b / NC, lane);
-            } else if constexpr (C == 4 && NC == 1) {
+            } else if constexpr ((C == 4 && NC == 1) || (C == 2 && NC == 2)) {
                 if (A.tr != 0)
-                    store_strip_tr<C, NC>(A, lds, B, b, lane);  // (row band in horizontal strips)
+                    store_strip_tr<C, NC>(A, lds, B, b % NC, b / NC, lane);  // (row band in horizontal strips)
                 else
-                    store_strip<C, NC>(A, lds, B, 0, b, lane);
+                    store_strip<C, NC>(A, lds, B, b % NC, b / NC, lane);
             } else {
                 store_strip<C, NC>(A, lds, B, b % NC, b / NC, lane);
             }

@@ -136,11 +136,13 @@ class LocalTBands:
     (nw_fill_tband_async): the mpi-horz partition and row-major band tables of
     LocalBands, each band swept as 256-row strips along the columns, band r-1's
     last row fed to band r column by column through a Feed(n1) buffer.  Each band
-    gets 1/P of the resident (4, 1) workers so that all bands are co-resident."""
+    gets 1/P of the resident workers so that all bands are co-resident.  shape: the
+    strip shape (C, NC), TBAND_SHAPE by default ((4, 1) or (2, 2))."""
 
-    def __init__(self, n1: int, n2: int, nbands: int, device: int = 0):
+    def __init__(self, n1: int, n2: int, nbands: int, device: int = 0, shape=None):
         import torch
         self.n1, self.n2, self.P, self.device = n1, n2, nbands, device
+        self.shape = tuple(shape) if shape else TBAND_SHAPE
         self.layout = plan(n2, nbands)
         if any(rows < 2 for rows, _ in self.layout):
             raise ValueError(f"{nbands} horizontal-strip bands need at least one row below each halo")
@@ -148,7 +150,7 @@ class LocalTBands:
         self.feeds = [None] + [nwhip.Feed(n1, device) for _ in range(nbands - 1)]
         self.ctxs = [nwhip.Context(device) for _ in range(nbands)]
         self.streams = [torch.cuda.Stream(device) for _ in range(nbands)]
-        self.waves = max(1, resident_waves(device, 4, 1) // nbands)
+        self.waves = max(1, resident_waves(device, *self.shape) // nbands)
         self.tag = 0
 
     def fill(self, d_s1, d_s2, scheme=(1, 0, -1), flags: int = 0, timeout_ms: int = 0) -> int:
@@ -163,7 +165,8 @@ class LocalTBands:
                 d_s1, d_s2[start:start + rows - 1], self.tables[r], row0=start,
                 feed_in=self.feeds[r].ptr if r > 0 else None,
                 feed_out=self.feeds[r + 1].ptr if r + 1 < self.P else None,
-                tag=self.tag, scheme=scheme, waves=self.waves, stream=st, flags=flags, timeout_ms=timeout_ms)
+                tag=self.tag, scheme=scheme, waves=self.waves, stream=st, flags=flags, timeout_ms=timeout_ms,
+                substrips=self.shape[0], strip_waves=self.shape[1])
         for r, st in enumerate(self.streams):
             s = self.ctxs[r].status(st)
             if s != nwhip.NW_OK:
@@ -426,7 +429,7 @@ def _sweep(args, partition: str, rank: int, world: int, dev: int, scheme, blocks
         s2 = torch.from_numpy(nwhip.synth(2, n2)[start:start + rows - 1].copy()).cuda()
         table = nwhip.Context.alloc_table(n1, rows - 1)
         links_in = [nwhip.Feed(n1, dev) for _ in range(2)] if rank > 0 else None
-        sub, nc = 4, 1
+        sub, nc = tband_shape(args)
         ncols = n1 + 1
     else:
         # row bands (mpi-horz, BASELINE config 4): rank r owns band_rows rows
@@ -484,7 +487,7 @@ def _sweep(args, partition: str, rank: int, world: int, dev: int, scheme, blocks
             elif hrows:
                 ctx.fill_tband(s1, s2, table, row0=start, feed_in=links_in[b].ptr if links_in else None,
                                feed_out=hout, tag=k, scheme=scheme, waves=waves, stream=stream,
-                               timeout_ms=timeout_ms)
+                               timeout_ms=timeout_ms, substrips=sub, strip_waves=nc)
             elif cyc:
                 ctx.fill_band_cycle(s1, s2, h, table, halo_in=links_in[b].ptr, halo_out=hout,
                                     hin_first=rank > 0, hout_shift=int(rank == world - 1), row0_max=start, **kw)
@@ -699,6 +702,22 @@ def check_ranks(ctx, link_word, rank: int, world: int, what: str) -> None:
 # main leg and measures 2 blocks per GPU (the only count the model finds no worse)
 # as an alternate.
 CYCLE_ALT_BLOCKS = 2
+
+
+# Strip shape of the horizontal sweep (nw_fill_tband_async): (4, 1) or (2, 2), both
+# 256 rows; bench.py --tband-shape overrides it.
+TBAND_SHAPE = (4, 1)
+
+
+def tband_shape(args) -> tuple:
+    """(C, NC) of the horizontal-strip row bands: --tband-shape "C,NC" or TBAND_SHAPE."""
+    v = getattr(args, "tband_shape", None)
+    if not v:
+        return TBAND_SHAPE
+    c, nc = (int(x) for x in str(v).split(","))
+    if (c, nc) not in ((4, 1), (2, 2)):
+        raise ValueError(f"--tband-shape {v}: horizontal strips take (4, 1) or (2, 2)")
+    return c, nc
 
 
 # A horizontal sweep runs its strips side by side along the whole width: a band of

@@ -404,7 +404,8 @@ int nw_fill_colband_async(nw_ctx *ctx, const int8_t *d_s1, int64_t n1, const int
  * feed_in (the boundary j*gap for band 0) and column 0 is the boundary i*gap.
  * d_t: (n2_band + 1) rows laid out like nw_table_offset's (column 1 starts a
  * 256-byte line), pitch >= nw_table_pitch(n1); d_s2_band: the band's n2_band side
- * characters (global rows row0 + 1 ..).  NW mode, strips (4, 1) only
+ * characters (global rows row0 + 1 ..).  NW mode, strip shapes (4, 1) (the default,
+ * nw_params.substrips = strip_waves = 0) and (2, 2) -- 256 rows either way
  * (NW_ERR_UNSUPPORTED otherwise).  Asynchronous on `stream`. */
 typedef struct nw_tband {
     const uint64_t *feed_in;  /* NULL: first band (row 0 = the boundary j*gap)     */

@@ -57,3 +57,46 @@ def test_two_passes_share_workers(tmp_path):
     for P, ms in t.items():
         want = ((P + 1) * d + (P - 1) * halo) / 1e3
         assert abs(ms - want) < 0.01 + 1e-3 * want, (P, ms, want)
+
+
+def _n8_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("n8_model", os.path.join(ROOT, "tools", "n8_model.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def test_family_bounds_closed_form():
+    """tools/n8_model.py --families on synthetic inputs: a horizontal
+    family is D + (S-1) h with D = max(band bytes / store rate, n1 x its sweep pace), a
+    vertical one max(7 tau + bytes / rate, (n1 / W - 1) h + 8 tau), and the bare hop
+    is NC x 63 steps of skew + (NC-1) LDS hand-offs + one memory hand-off."""
+    m = _n8_module()
+    inp = {"clock_ghz": 2.0, "store_tbps": 6.0, "gran_rows": 16, "mem_handoff_us": 3.0, "lds_handoff_us": 0.5,
+           "step_cycles": {"4,1": 100.0, "2,2": 60.0},
+           "infill": {"4,1": {"hop_us": 10.0, "leader_ns_per_row": 50.0, "follower_ns_per_row": 40.0}},
+           "panel_row_ns": {"bare": 100.0, "infill": 100.0}, "scan_step_ns_1wave": {"bare": 90.0, "infill": 90.0}}
+    d_store = m.band_bytes() / 6.0e12 * 1e3
+    bare = {f: t for f, _, t, _ in m.family_bounds(inp, "bare")}
+    h41 = (63 * 50.0 + 16 * 50.0) * 1e-3 + 3.0          # step 50 ns
+    assert abs(bare["H(4,1)"] - (max(d_store, 524288 * 50e-6) + 2047 * h41 * 1e-3)) < 1e-9
+    h22 = (2 * 63 * 30.0 + (16 * 30.0) * 2) * 1e-3 + 0.5 + 3.0  # step 30 ns, one LDS hand-off
+    assert abs(bare["H(2,2)"] - (d_store + 2047 * h22 * 1e-3)) < 1e-9
+    tau = 65536 * 30.0 * 1e-6
+    assert abs(bare["V(2,2)"] - max(7 * tau + d_store, 2047 * h22 * 1e-3 + 8 * tau)) < 1e-9
+    fill = {f: t for f, _, t, _ in m.family_bounds(inp, "infill")}
+    assert abs(fill["H(4,1)"] - (max(d_store, 524288 * 40e-6) + 2047 * 10.0e-3)) < 1e-9
+    assert abs(fill["V(4,1)"] - max(7 * 65536 * 50e-6 + d_store, 2047 * 10.0e-3 + 8 * 65536 * 50e-6)) < 1e-9
+    assert abs(m.target_ms(45.064) - 30.04) < 0.01
+
+
+def test_family_table_runs_on_committed_inputs():
+    """The committed inputs (profiles/n8_inputs.json, every number with its source) give
+    the table DESIGN.md section 5 quotes: no in-fill family reaches the 6x line."""
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "n8_model.py"), "--families"],
+                         capture_output=True, text=True, check=True).stdout
+    assert "needs <= 30.04 ms per fill" in out
+    rows = re.findall(r"^(\S+)\s+.*?\s([0-9.]+)ms\s+([0-9.]+)ms", out, re.M)
+    assert len(rows) >= 12
+    assert min(float(r[2]) for r in rows) > 30.04

@@ -56,11 +56,14 @@ def test_row_band_is_the_transposed_column_band(n1, n2, P, scheme):
         np.testing.assert_array_equal(oracle.fill_band(s1, s2, P, r, halo, scheme), full[start:start + rows])
 
 
-def _check(torch, n1, n2, P, scheme, seed, alphabet=4):
+SHAPES = [(4, 1), (2, 2)]  # the horizontal strip shapes (256 rows each)
+
+
+def _check(torch, n1, n2, P, scheme, seed, alphabet=4, shape=(4, 1)):
     rng = np.random.default_rng(seed)
     s1 = rng.integers(1, alphabet + 1, n1).astype(np.int8)
     s2 = rng.integers(1, alphabet + 1, n2).astype(np.int8)
-    tb = nw_bands.LocalTBands(n1, n2, P)
+    tb = nw_bands.LocalTBands(n1, n2, P, shape=shape)
     try:
         score = tb.fill(torch.from_numpy(s1).cuda(), torch.from_numpy(s2).cuda(), scheme)
         full = oracle.fill(s1, s2, scheme)
@@ -77,27 +80,31 @@ def _check(torch, n1, n2, P, scheme, seed, alphabet=4):
                                      (129, 40, 1), (64 * 37 + 5, 999, 5), (5, 600, 3), (4100, 1300, 2),
                                      (33, 257, 1), (1, 513, 2), (2000, 20, 8), (97, 1025, 4)])
 @pytest.mark.parametrize("scheme", [(1, 0, -1), (1, -1, -1), (2, -1, -2)])
-def test_local_tbands_vs_oracle(torch_gpu, n1, n2, P, scheme):
+@pytest.mark.parametrize("shape", SHAPES, ids=["4x1", "2x2"])
+def test_local_tbands_vs_oracle(torch_gpu, n1, n2, P, scheme, shape):
     """Partial first/last strips, bands of a few rows, 1-column tables, widths that are
     not a multiple of the 32-column store batch; the v_perm form (scores - 2 GAP
-    in int8) and the compare forms (UNIT: match - mismatch == 1, GEN: (2,-1,-2))."""
-    _check(torch_gpu, n1, n2, P, scheme, n1 * 31 + n2 + P)
+    in int8) and the compare forms (UNIT: match - mismatch == 1, GEN: (2,-1,-2)); both
+    strip shapes ((2, 2): the band's last row may sit in either compute wave's ring)."""
+    _check(torch_gpu, n1, n2, P, scheme, n1 * 31 + n2 + P, shape=shape)
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("scheme", [(1, 0, -1), (3, -2, -1), (1, -1, 0), (2, 1, 1)])
-def test_local_tbands_alphabets_and_schemes(torch_gpu, scheme):
+@pytest.mark.parametrize("shape", SHAPES, ids=["4x1", "2x2"])
+def test_local_tbands_alphabets_and_schemes(torch_gpu, scheme, shape):
     """More than kMaxPerm distinct row characters (the compare fallback), gap 0 and a
     positive gap."""
-    _check(torch_gpu, 700, 900, 3, scheme, 5, alphabet=20)
+    _check(torch_gpu, 700, 900, 3, scheme, 5, alphabet=20, shape=shape)
 
 
 @pytest.mark.gpu
-def test_local_tbands_repeated_launches(torch_gpu):
+@pytest.mark.parametrize("shape", SHAPES, ids=["4x1", "2x2"])
+def test_local_tbands_repeated_launches(torch_gpu, shape):
     """Tags advance per launch; stale feed granules of earlier launches are never taken."""
     torch = torch_gpu
     n1, n2, P = 2000, 1500, 3
-    tb = nw_bands.LocalTBands(n1, n2, P)
+    tb = nw_bands.LocalTBands(n1, n2, P, shape=shape)
     try:
         for seed in range(4):
             rng = np.random.default_rng(seed)
@@ -114,12 +121,13 @@ def test_local_tbands_repeated_launches(torch_gpu):
 
 
 @pytest.mark.gpu
-def test_local_tbands_32k_score(torch_gpu):
+@pytest.mark.parametrize("shape", SHAPES, ids=["4x1", "2x2"])
+def test_local_tbands_32k_score(torch_gpu, shape):
     """BASELINE config-2 inputs split into 4 concurrent horizontal-strip bands."""
     torch = torch_gpu
     n = 32768
     s1, s2 = nwhip.synth(1, n), nwhip.synth(2, n)
-    tb = nw_bands.LocalTBands(n, n, 4)
+    tb = nw_bands.LocalTBands(n, n, 4, shape=shape)
     try:
         score = tb.fill(torch.from_numpy(s1).cuda(), torch.from_numpy(s2).cuda())
         assert score == 13394  # reference serial.cpp on the same inputs (synth_scores.json)
@@ -167,6 +175,10 @@ def test_tband_refusals(torch_gpu):
             if st != nwhip.NW_OK:
                 raise nwhip.NwError(st, "nw_fill_tband_async")
         assert e.value.status == nwhip.NW_ERR_UNSUPPORTED
+        for sub, nc in [(1, 4), (2, 1), (1, 1), (2, 4), (4, 2)]:  # 256-row (4, 1) / (2, 2) strips only
+            with pytest.raises(nwhip.NwError) as e:
+                ctx.fill_tband(s1, s2, tab, substrips=sub, strip_waves=nc)
+            assert e.value.status in (nwhip.NW_ERR_UNSUPPORTED, nwhip.NW_ERR_ARG), (sub, nc)
         torch.cuda.synchronize()
         ctx.fill_tband(s1, s2, tab)  # and the context still works
         torch.cuda.synchronize()
@@ -178,7 +190,7 @@ def test_tband_refusals(torch_gpu):
 
 
 # ------------------------------------------------------------------ the row-scan finisher
-def _tband_chain(torch, s1, s2, P, scheme, waves, flags=0, row_split=None):
+def _tband_chain(torch, s1, s2, P, scheme, waves, flags=0, row_split=None, shape=(4, 1)):
     """P bands of the (s1, s2) table, each filled by its own nw_fill_tband_async with
     `waves` workers, one after the other on one stream (band r's feed_out is band r+1's
     feed_in).  Returns (band tables, [published feed of band r]) as numpy."""
@@ -196,7 +208,7 @@ def _tband_chain(torch, s1, s2, P, scheme, waves, flags=0, row_split=None):
             d2 = torch.from_numpy(s2[start:start + rows - 1].copy()).cuda()
             ctx.fill_tband(d1, d2, tab, row0=start, feed_in=feeds[r - 1] if r > 0 else None,
                            feed_out=feeds[r] if r + 1 < P else None, tag=5, scheme=scheme, waves=waves,
-                           flags=flags)
+                           flags=flags, substrips=shape[0], strip_waves=shape[1])
             torch.cuda.synchronize()
             assert ctx.status() == nwhip.NW_OK, f"band {r}: {ctx.debug_failure()}"
             out.append(tab[:rows, :n1 + 1].cpu().numpy())
@@ -210,7 +222,8 @@ def _tband_chain(torch, s1, s2, P, scheme, waves, flags=0, row_split=None):
 @pytest.mark.gpu
 @pytest.mark.parametrize("n1", [1, 100, 2047, 2048, 2049, 5000])
 @pytest.mark.parametrize("waves,extra", [(1, 1), (2, 7), (2, 64), (3, 200), (1, 256), (4, 129)])
-def test_tband_finisher_rows(torch_gpu, n1, waves, extra):
+@pytest.mark.parametrize("shape", SHAPES, ids=["4x1", "2x2"])
+def test_tband_finisher_rows(torch_gpu, n1, waves, extra, shape):
     """A band whose last strip would run alone as one more pass over all columns
     (strips = k * workers + 1) leaves that strip's rows (`extra` of them) to the
     row-scan finisher (nw_finish.hip): one prefix-max scan per row across the width,
@@ -225,7 +238,7 @@ def test_tband_finisher_rows(torch_gpu, n1, waves, extra):
     for scheme in [(1, 0, -1), (1, -1, -1), (2, -1, -2)]:
         full = oracle.fill(s1, s2, scheme)
         split = [(R + 1, 0), (R + 1, R)]  # two bands of R computed rows each, the second below a halo
-        tabs, pub = _tband_chain(torch, s1, s2, 2, scheme, waves, row_split=split)
+        tabs, pub = _tband_chain(torch, s1, s2, 2, scheme, waves, row_split=split, shape=shape)
         for r, (rows, start) in enumerate(split):
             np.testing.assert_array_equal(tabs[r], full[start:start + rows], err_msg=f"band {r} {scheme}")
         gap = scheme[2]
@@ -275,9 +288,10 @@ def test_tband_finisher_matches_full_pass(torch_gpu):
 
 
 @pytest.mark.gpu
-def test_local_tbands_leftover_row(torch_gpu):
+@pytest.mark.parametrize("shape", SHAPES, ids=["4x1", "2x2"])
+def test_local_tbands_leftover_row(torch_gpu, shape):
     """The mpi-horz partition's leftover row (bands after the first carry their halo
     row, the last one the remainder): 2 bands sharing the GPU (each 1/2 of the workers),
     the second sweeping 32769 rows = 129 strips on 128 workers -- the configuration that
     ran a second full pass before the finisher."""
-    _check(torch_gpu, 300, 65537, 2, (1, 0, -1), 3)
+    _check(torch_gpu, 300, 65537, 2, (1, 0, -1), 3, shape=shape)

@@ -18,8 +18,10 @@ ap.add_argument("--n1", type=int, default=524288)
 ap.add_argument("--n2", type=int, default=65536)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--flags", type=int, default=0, help="nw_params.flags (513 = 0x201: timing only + no store waves, the compute pace)")
+ap.add_argument("--shape", default="4,1", help="horizontal strip shape C,NC: 4,1 or 2,2")
 ap.add_argument("--vertical", default="4:1,2:2", help="vertical-strip shapes to time beside it ('' = none)")
 args = ap.parse_args()
+SC, SNC = (int(x) for x in args.shape.split(","))
 ctx = nwhip.Context(0)
 s1 = torch.from_numpy(nwhip.synth(1, args.n1)).cuda()
 s2 = torch.from_numpy(nwhip.synth(2, args.n2)).cuda()
@@ -41,7 +43,7 @@ tag = [0]
 
 def tband():
     tag[0] += 1
-    ctx.fill_tband(s1, s2, tab, tag=tag[0], flags=args.flags)
+    ctx.fill_tband(s1, s2, tab, tag=tag[0], flags=args.flags, substrips=SC, strip_waves=SNC)
 
 
 timed(tband)
@@ -51,7 +53,7 @@ ms = min(ts)
 strips = -(-args.n2 // 256)
 pace = ms * 1e6 / (args.n1 + (strips - 1) * 64)
 score = int(tab[args.n2, args.n1].item())
-print(f"horizontal {args.n1}x{args.n2} flags={args.flags} ms={ms:.3f} GCUPS={args.n1 * args.n2 / (ms * 1e6):.1f} "
+print(f"horizontal ({SC},{SNC}) {args.n1}x{args.n2} flags={args.flags} ms={ms:.3f} GCUPS={args.n1 * args.n2 / (ms * 1e6):.1f} "
       f"pace={pace:.1f}ns/col score={score} all={[round(t, 2) for t in ts]}", flush=True)
 for sh in [x for x in args.vertical.split(",") if x]:
     c, nc = (int(x) for x in sh.split(":"))

@@ -15,7 +15,9 @@ import nwhip  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--n1", type=int, default=524288)
 ap.add_argument("--n2", default="16384,65536")
+ap.add_argument("--shape", default="4,1", help="horizontal strip shape C,NC: 4,1 or 2,2")
 args = ap.parse_args()
+SC, SNC = (int(x) for x in args.shape.split(","))
 ctx = nwhip.Context(0)
 s1 = torch.from_numpy(nwhip.synth(1, args.n1)).cuda()
 for n2 in [int(x) for x in args.n2.split(",")]:
@@ -23,18 +25,18 @@ for n2 in [int(x) for x in args.n2.split(",")]:
     tab = nwhip.Context.alloc_table(args.n1, n2)
     nstrips = -(-n2 // 256)
     tr = torch.zeros(nstrips * 24, dtype=torch.int64, device="cuda")
-    ctx.fill_tband(s1, s2, tab, tag=1)
+    ctx.fill_tband(s1, s2, tab, tag=1, substrips=SC, strip_waves=SNC)
     ctx.set_trace(tr)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    ctx.fill_tband(s1, s2, tab, tag=2)
+    ctx.fill_tband(s1, s2, tab, tag=2, substrips=SC, strip_waves=SNC)
     e1.record()
     torch.cuda.synchronize()
     ctx.set_trace(None)
     t = tr.view(nstrips, 24).cpu().numpy().astype(np.float64)
     t0 = t[:, 0].min()
     st, en = (t[:, 0] - t0) / 100.0, (t[:, 1] - t0) / 100.0
-    print(f"{args.n1}x{n2} strips={nstrips} ms={e0.elapsed_time(e1):.3f} span_us={en.max():.0f}")
+    print(f"({SC},{SNC}) {args.n1}x{n2} strips={nstrips} ms={e0.elapsed_time(e1):.3f} span_us={en.max():.0f}")
     for col, nm in ((4, "quarter"), (5, "mid")):
         hop = np.diff(t[:, col]) / 100.0
         print(f"  hop at {nm} (us): med {np.median(hop):.2f} p10 {np.percentile(hop, 10):.2f} "
@@ -43,6 +45,18 @@ for n2 in [int(x) for x in args.n2.split(",")]:
     dur = en - st
     print(f"  strip duration (us): first {dur[0]:.0f} med {np.median(dur):.0f} max {dur.max():.0f}; "
           f"end of last {en[-1]:.0f}")
+    # the chain accumulates the MEAN strip-to-strip lag, rare stalls included: the end
+    # lags, and where the largest ones arose (a stall shifts every strip below it)
+    lag = np.diff(en)
+    hq, hm = np.diff(t[:, 4]) / 100.0, np.diff(t[:, 5]) / 100.0
+    print(f"  end lag (us): mean {lag.mean():.2f} (= (end of last - end of first) / {nstrips - 1}) med "
+          f"{np.median(lag):.2f} p99 {np.percentile(lag, 99):.1f} max {lag.max():.1f}; lags > 50 us: "
+          f"{int((lag > 50).sum())}, their sum {lag[lag > 50].sum():.0f} us")
+    for k in np.argsort(-np.maximum(np.maximum(lag, hq), hm))[:6]:
+        s = k + 1
+        print(f"   strip {s}: end lag {lag[k]:.1f} hop quarter {hq[k]:.1f} mid {hm[k]:.1f} us; feed waits "
+              f"{t[s, 2]:.0f} ({t[s, 3] / 100:.0f} us); ring-space wait first/last wave {t[s, 11] / 100:.0f} / "
+              f"{t[s, 12] / 100:.0f} us; its producer's ring wait {t[k, 11] / 100:.0f} / {t[k, 12] / 100:.0f} us")
     print(f"  feed waits / strip: med {np.median(t[:, 2]):.0f} max {t[:, 2].max():.0f}; wait us med "
           f"{np.median(t[:, 3]) / 100:.0f} max {t[:, 3].max() / 100:.0f}; ring-space wait us (last wave) med "
           f"{np.median(t[:, 12]) / 100:.0f}", flush=True)
