@@ -652,6 +652,8 @@ int nw_fill_colband_async(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_
 // symmetric), in global row numbers: its "columns" are global rows row0 + 1 ..
 // row0 + R (strips of 256 rows from row0 + 1), its "rows" the band's columns
 // 0..n1; the store waves write the row-major band table (store_strip_tr).
+static constexpr int kTbandLeadSleep = 8;
+
 int nw_fill_tband_async(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t *d_s2, int64_t R,
                         const nw_params *p, const nw_tband *tb, int32_t *d_t, int64_t pitch, void *stream) {
     if (!c || !d_t || !tb || !d_s1 || !d_s2 || n1 < 1 || R < 1 || n1 >= INT32_MAX || R >= INT32_MAX ||
@@ -761,6 +763,16 @@ int nw_fill_tband_async(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t 
             return e != nullptr && e[0] == '1';
         }();
         a.tr_store_pub = compute_pub && tNC == 1 ? 0 : 1;  // ((2, 2): the store waves publish)
+        // the band's unfed leading strip (band 0's strip 0: the whole chain's leader)
+        // sleeps 8 x 64 clocks per 64-step iteration (~8 %): followers that run 1-2 %
+        // slower for a while then keep up instead of delaying every strip below them
+        // (mean strip-to-strip lag 16.3-17.4 -> 12.5 us, leader 25.8 -> 27.5-28.0 ms;
+        // profiles/r06f_lead_sleep.txt); NW_LEAD_SLEEP overrides (A/B, 0 = off)
+        static const int lead_sleep = [] {
+            const char *e = std::getenv("NW_LEAD_SLEEP");
+            return e != nullptr ? std::atoi(e) : kTbandLeadSleep;
+        }();
+        a.lead_sleep = tNC == 1 ? lead_sleep : 0;
     }
     if (nw::launch_fill(a, tC, tNC, (int)s.waves, stream) != hipSuccess) return NW_ERR_HIP;
     if (nw::launch_tband_edges(tb->feed_in, d_t, pitch, n1, R + 1, p->gap, tb->row0, stream) != hipSuccess)

@@ -91,6 +91,9 @@ struct FillArgs {
     int32_t tr_store_pub;  // 1: the last strip's store waves publish the band's last row
                            // (0: its compute wave, NW_TR_PUB_COMPUTE=1 for A/B)
     int64_t tr_y0;
+    // the unfed leading strip sleeps lead_sleep x 64 clocks per 64-step iteration
+    // (horizontal (4, 1) strips: 8, nw_capi.cpp kTbandLeadSleep; NW_LEAD_SLEEP overrides)
+    int32_t lead_sleep;
 };
 bool sw_shape_ok(int substrips, int strip_waves);
 // column band r > 0: local column 0 (global column `start`) from the feed

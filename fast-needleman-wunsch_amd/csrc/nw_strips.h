@@ -788,6 +788,10 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
                 F.ready = min(64 / G, (pv - it * 64) / G);
                 lds_order();  // feed reads after the counter that published them
             } else {
+                // the unfed leader of a horizontal band sleeps a little per iteration
+                // (FillArgs::lead_sleep), so that a follower that runs slower for a
+                // while keeps up instead of delaying every strip below it
+                for (int z = 0; z < A.lead_sleep; ++z) __builtin_amdgcn_s_sleep(1);
                 // strip 0, wave 0: left of column col0 is the boundary column:
                 // w[r][0] = t[r][0] - GAP*r = t[0][0] with col0 = 1, "minus infinity"
                 // when col0 = 0 (the lane holding column 0 then computes
