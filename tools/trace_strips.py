@@ -12,6 +12,7 @@ import nwhip  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=32768)
+ap.add_argument("--n1", type=int, default=0, help="columns (default: --n, a square); e.g. 256 = one strip alone")
 ap.add_argument("--waves", default="0")
 ap.add_argument("--flags", type=int, default=0)
 ap.add_argument("--sub", type=int, default=0)
@@ -21,10 +22,11 @@ ap.add_argument("--sw", action="store_true", help="Smith-Waterman mode, scheme (
 args = ap.parse_args()
 ctx = nwhip.Context(0)
 n = args.n
-s1 = torch.from_numpy(nwhip.synth(1, n)).cuda()
+n1 = args.n1 or n
+s1 = torch.from_numpy(nwhip.synth(1, n1)).cuda()
 s2 = torch.from_numpy(nwhip.synth(2, n)).cuda()
-tab = nwhip.Context.alloc_table(n, n)
-nstrips = (n + 1 + 63) // 64
+tab = nwhip.Context.alloc_table(n1, n)
+nstrips = max(2, (n1 + 1 + 63) // 64)
 tr = torch.zeros(nstrips * 24, dtype=torch.int64, device="cuda")
 for w in [int(x) for x in args.waves.split(",")]:
     ctx.set_trace(None)
@@ -80,7 +82,8 @@ for w in [int(x) for x in args.waves.split(",")]:
     print(f"  busy ns/row: strip0 {busy_row[0]:.2f} med {np.median(busy_row):.2f} p90 {np.percentile(busy_row, 90):.2f}")
     print(f"  strip duration us: min {dur.min():.0f} med {np.median(dur):.0f} max {dur.max():.0f}"
           f"  -> per row {np.median(dur)/n*1000:.2f} ns")
-    print(f"  start lag us: med {np.median(lag):.2f} p10 {np.percentile(lag,10):.2f} p90 {np.percentile(lag,90):.2f}")
+    if lag.size:
+        print(f"  start lag us: med {np.median(lag):.2f} p10 {np.percentile(lag,10):.2f} p90 {np.percentile(lag,90):.2f}")
     print(f"  slow waits/strip: med {np.median(t[:,2]):.0f} max {t[:,2].max():.0f}; wait us/strip med "
           f"{np.median(t[:,3])/100:.0f} max {t[:,3].max()/100:.0f}")
     print(f"  ring back-pressure us/strip: first wave med {np.median(t[:,11])/100:.0f} "
@@ -89,7 +92,7 @@ for w in [int(x) for x in args.waves.split(",")]:
     cyc = (t[:, 7] - t[:, 6])
     print(f"  cycles/step inside run_iter: first wave strip0 {t[0,14]/n:.1f} med {np.median(t[:,14])/n:.1f}; "
           f"last wave strip0 {t[0,15]/n:.1f} med {np.median(t[:,15])/n:.1f}; whole strip med {np.median(cyc)/n:.1f}")
-    for q in [0, 1, 2, nstrips // 4, nstrips // 4 + 1, nstrips // 2, nstrips - 2, nstrips - 1]:
+    for q in sorted({min(x, nstrips - 1) for x in [0, 1, 2, nstrips // 4, nstrips // 4 + 1, nstrips // 2, nstrips - 2, nstrips - 1]}):
         print(f"   strip {q}: start {st[q]:.1f} end {en[q]:.1f} dur {dur[q]:.1f} slow {t[q,2]:.0f} wait {t[q,3]/100:.1f} "
               f"ringwait first {t[q,11]/100:.0f} last {t[q,12]/100:.0f} lastfeed {t[q,13]/100:.0f} "
               f"run_iter cyc/step first {t[q,14]/n:.1f} last {t[q,15]/n:.1f} "
