@@ -669,6 +669,7 @@ int nw_fill_tband_async(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t 
         if (!((tC == 4 && tNC == 1) || (tC == 2 && tNC == 2))) return NW_ERR_UNSUPPORTED;
     }
     if (tb->tag == 0 || (((uintptr_t)tb->feed_in | (uintptr_t)tb->feed_out) & 7u) != 0) return NW_ERR_ARG;
+    if ((tb->flags & ~(uint32_t)NW_TBAND_DENSE_POLLS) != 0) return NW_ERR_ARG;
     if ((tb->row0 > 0) != (tb->feed_in != nullptr)) return NW_ERR_ARG;
     if (tb->feed_out && (p->flags & 1)) return NW_ERR_ARG;  // needs the real last row
     if ((p->flags & NW_FLAG_DEBUG_NO_CHAIN) && (tb->feed_in || tb->feed_out)) return NW_ERR_ARG;  // (no fill to hand on)
@@ -773,6 +774,7 @@ int nw_fill_tband_async(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t 
             return e != nullptr ? std::atoi(e) : kTbandLeadSleep;
         }();
         a.lead_sleep = tNC == 1 ? lead_sleep : 0;
+        a.tr_dense = (tb->flags & NW_TBAND_DENSE_POLLS) != 0 ? 1 : 0;
     }
     if (nw::launch_fill(a, tC, tNC, (int)s.waves, stream) != hipSuccess) return NW_ERR_HIP;
     if (nw::launch_tband_edges(tb->feed_in, d_t, pitch, n1, R + 1, p->gap, tb->row0, stream) != hipSuccess)

@@ -94,6 +94,8 @@ struct FillArgs {
     // the unfed leading strip sleeps lead_sleep x 64 clocks per 64-step iteration
     // (horizontal (4, 1) strips: 8, nw_capi.cpp kTbandLeadSleep; NW_LEAD_SLEEP overrides)
     int32_t lead_sleep;
+    // horizontal strips: 1 = waiting strips poll with s_sleep 1 (NW_TBAND_DENSE_POLLS)
+    int32_t tr_dense;
 };
 bool sw_shape_ok(int substrips, int strip_waves);
 // column band r > 0: local column 0 (global column `start`) from the feed

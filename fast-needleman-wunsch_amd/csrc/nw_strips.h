@@ -289,6 +289,9 @@ struct Lanes {
 // 30.6 -> 28.4 ms and 2 chained bands 31.3-33.3 -> 30.1-31.0 ms at a hop of 12.3
 // instead of 11.5 us (profiles/r05y_poll_sleep.txt).  The vertical sweeps and
 // the SW fill, whose chains are latency-bound, lose with it and keep 1.
+// (Round 6, with the chain's leader throttled, profiles/r06l_poll_sleep.txt: 1 / 16 /
+// 32 / 64 give a mean lag of 9.9 / 10.8 / 11.7 / 12.4 us at a leader of 29.4 / 28.3 /
+// 28.1 / 27.0 ms -- so a launch may ask for dense polls, NW_TBAND_DENSE_POLLS.)
 constexpr int kPollSleepTr = 64;
 
 // Where a compute wave's feed comes from.
@@ -675,9 +678,10 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
     F.trace_pub = false;
     F.tpub = 0;
     F.tmo = A.timeout_ticks;
-    // sparse polls (kPollSleepTr) for the (4, 1) horizontal strips only: the (2, 2)
+    // sparse polls (kPollSleepTr) for the (4, 1) horizontal strips only, unless the
+    // launch asks for dense ones (NW_TBAND_DENSE_POLLS: long chains, r06l): the (2, 2)
     // ones poll with them at a 24 us hop, with s_sleep 1 at 11 us (profiles/r06c_tband22.txt)
-    F.sparse = A.tr != 0 && NC == 1;
+    F.sparse = A.tr != 0 && NC == 1 && A.tr_dense == 0;
     Out O;
     O.lds = j + 1 < NC;
     O.off = !O.lds && ((A.tr != 0 && feeds && A.tr_store_pub != 0 && (A.flags & 1) == 0) || nochain);

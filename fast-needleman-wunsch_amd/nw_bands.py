@@ -139,10 +139,11 @@ class LocalTBands:
     gets 1/P of the resident workers so that all bands are co-resident.  shape: the
     strip shape (C, NC), TBAND_SHAPE by default ((4, 1) or (2, 2))."""
 
-    def __init__(self, n1: int, n2: int, nbands: int, device: int = 0, shape=None):
+    def __init__(self, n1: int, n2: int, nbands: int, device: int = 0, shape=None, dense_polls: bool = False):
         import torch
         self.n1, self.n2, self.P, self.device = n1, n2, nbands, device
         self.shape = tuple(shape) if shape else TBAND_SHAPE
+        self.dense_polls = dense_polls
         self.layout = plan(n2, nbands)
         if any(rows < 2 for rows, _ in self.layout):
             raise ValueError(f"{nbands} horizontal-strip bands need at least one row below each halo")
@@ -166,7 +167,7 @@ class LocalTBands:
                 feed_in=self.feeds[r].ptr if r > 0 else None,
                 feed_out=self.feeds[r + 1].ptr if r + 1 < self.P else None,
                 tag=self.tag, scheme=scheme, waves=self.waves, stream=st, flags=flags, timeout_ms=timeout_ms,
-                substrips=self.shape[0], strip_waves=self.shape[1])
+                substrips=self.shape[0], strip_waves=self.shape[1], dense_polls=self.dense_polls)
         for r, st in enumerate(self.streams):
             s = self.ctxs[r].status(st)
             if s != nwhip.NW_OK:
@@ -396,6 +397,7 @@ def _sweep(args, partition: str, rank: int, world: int, dev: int, scheme, blocks
     kernel = getattr(args, "kernel", 0) if not hrows else nwhip.KERNEL_STRIPS
     m = max(1, blocks) if partition == "rows" else 1
     cyc = m > 1
+    dense = False  # (horizontal strips: follower polls, tband_dense)
     ctx = nwhip.Context(dev)
     stream = torch.cuda.current_stream()
     h = 0
@@ -430,6 +432,7 @@ def _sweep(args, partition: str, rank: int, world: int, dev: int, scheme, blocks
         table = nwhip.Context.alloc_table(n1, rows - 1)
         links_in = [nwhip.Feed(n1, dev) for _ in range(2)] if rank > 0 else None
         sub, nc = tband_shape(args)
+        dense = tband_dense(args, n2)
         ncols = n1 + 1
     else:
         # row bands (mpi-horz, BASELINE config 4): rank r owns band_rows rows
@@ -487,7 +490,7 @@ def _sweep(args, partition: str, rank: int, world: int, dev: int, scheme, blocks
             elif hrows:
                 ctx.fill_tband(s1, s2, table, row0=start, feed_in=links_in[b].ptr if links_in else None,
                                feed_out=hout, tag=k, scheme=scheme, waves=waves, stream=stream,
-                               timeout_ms=timeout_ms, substrips=sub, strip_waves=nc)
+                               timeout_ms=timeout_ms, substrips=sub, strip_waves=nc, dense_polls=dense)
             elif cyc:
                 ctx.fill_band_cycle(s1, s2, h, table, halo_in=links_in[b].ptr, halo_out=hout,
                                     hin_first=rank > 0, hout_shift=int(rank == world - 1), row0_max=start, **kw)
@@ -570,7 +573,8 @@ def _sweep(args, partition: str, rank: int, world: int, dev: int, scheme, blocks
     del table
     torch.cuda.empty_cache()
     return {"wall": wall, "wall_pipe": wall_pipe, "fills": fills, "status": status, "link_status": link_status,
-            "failure": failure, "kms": kms, "score": score, "n1": n1, "n2": n2, "shape": [sub, nc], "kernel": kernel, "rows": rows,
+            "failure": failure, "kms": kms, "score": score, "n1": n1, "n2": n2, "shape": [sub, nc], "kernel": kernel,
+            "dense_polls": dense, "rows": rows,
             "start": start, "blocks": m, "block_rows": h}
 
 
@@ -702,6 +706,26 @@ def check_ranks(ctx, link_word, rank: int, world: int, what: str) -> None:
 # main leg and measures 2 blocks per GPU (the only count the model finds no worse)
 # as an alternate.
 CYCLE_ALT_BLOCKS = 2
+
+
+# Follower polls of the horizontal sweep (NW_TBAND_DENSE_POLLS; DESIGN.md section 5,
+# profiles/r06l_poll_sleep.txt): with the chain's leader throttled, s_sleep 1 polls give a
+# mean strip-to-strip lag of 9.9-10.3 us against 12.2-12.5 for s_sleep 64, but slow the
+# leader (29.4-30.0 vs 26.8-27.2 ms): they pay for chains longer than the break-even of
+# 2.4-2.9 ms / 2.2-2.5 us = 960-1300 strips of 256 rows -- N = 8 at 65536 rows per GPU
+# (2048 strips: -1.7 to -2.7 ms per fill), not N = 4 (1024: even).
+DENSE_POLL_STRIPS = 1200
+
+
+def tband_dense(args, n2: int) -> bool:
+    """Dense polls for a horizontal sweep of n2 rows in all: --tband-polls dense / sparse, or
+    auto (the default) = the chain of n2 / 256 strips is at least DENSE_POLL_STRIPS long."""
+    v = getattr(args, "tband_polls", None) or "auto"
+    if v not in ("auto", "dense", "sparse"):
+        raise ValueError(f"--tband-polls {v}: auto, dense or sparse")
+    if v != "auto":
+        return v == "dense"
+    return n2 // HSTRIP_ROWS >= DENSE_POLL_STRIPS
 
 
 # Strip shape of the horizontal sweep (nw_fill_tband_async): (4, 1) or (2, 2), both
@@ -902,6 +926,8 @@ def _line(args, world: int, scheme, part: str, ms: list) -> dict:
                               "horizontal strips of 256 rows (nw_fill_tband_async)",
                "halo": "in-kernel xGMI peer stores of the band's last row, 16 columns at a time, as the band's "
                        "last strip produces it",
+               "polls": ("dense (s_sleep 1)" if m0.get("dense_polls") else "sparse (s_sleep 64)") +
+                        ", the chain's leader throttled",
                **common}
     elif m0["blocks"] > 1:
         cfg = {"workload": f"nw_fill_rowbands_{n2}x{n1}", "band_rows": args.band_rows,

@@ -86,7 +86,10 @@ class NwColBand(ctypes.Structure):
 class NwTBand(ctypes.Structure):
     """nw_tband (include/nw_hip.h): feed granule buffers of one row band in horizontal strips."""
     _fields_ = [("feed_in", ctypes.c_void_p), ("feed_out", ctypes.c_void_p), ("tag", ctypes.c_uint32),
-                ("reserved", ctypes.c_uint32), ("row0", ctypes.c_int64)]
+                ("flags", ctypes.c_uint32), ("row0", ctypes.c_int64)]
+
+
+TBAND_DENSE_POLLS = 1  # nw_tband.flags NW_TBAND_DENSE_POLLS
 
 
 class NwError(RuntimeError):
@@ -675,14 +678,16 @@ class Context:
 
     def fill_tband(self, d_s1, d_s2_band, table, row0: int = 0, feed_in=None, feed_out=None, tag: int = 1,
                    scheme=(1, 0, -1), waves: int = 0, stream=None, flags: int = 0,
-                   timeout_ms: int = 0, substrips: int = 0, strip_waves: int = 0) -> None:
+                   timeout_ms: int = 0, substrips: int = 0, strip_waves: int = 0,
+                   dense_polls: bool = False) -> None:
         """Launch one row band in horizontal strips (asynchronous, nw_fill_tband_async):
         the nw_fill_band contract (table: alloc_table(n1, len(d_s2_band)), row 0 =
         global row `row0` = the previous band's last row) with the band's rows swept
         as 256-row strips along the columns.  feed_in / feed_out: Feed(n1) buffers'
         addresses (raw ints, e.g. peer memory from ipc_open_handle), int64 CUDA tensors
         of feed_bytes(n1) / 8 granules, or None at the ends.  (substrips, strip_waves):
-        the strip shape, (4, 1) (default) or (2, 2)."""
+        the strip shape, (4, 1) (default) or (2, 2).  dense_polls: NW_TBAND_DENSE_POLLS
+        (waiting strips poll with s_sleep 1: for chains of 1000+ strips)."""
         import torch
         n1, n2 = int(d_s1.numel()), int(d_s2_band.numel())
         assert table.dtype == torch.int32 and table.is_contiguous()
@@ -695,7 +700,7 @@ class Context:
             return x.data_ptr()
         if stream is None:
             stream = torch.cuda.current_stream(table.device)
-        b = NwTBand(addr(feed_in), addr(feed_out), int(tag), 0, int(row0))
+        b = NwTBand(addr(feed_in), addr(feed_out), int(tag), TBAND_DENSE_POLLS if dense_polls else 0, int(row0))
         p = params(scheme, waves, self.device, flags, substrips, strip_waves, timeout_ms)
         st = lib().nw_fill_tband_async(self._h, ctypes.c_void_p(d_s1.data_ptr() if n1 else 0), n1,
                                        ctypes.c_void_p(d_s2_band.data_ptr() if n2 else 0), n2, ctypes.byref(p),

@@ -59,11 +59,11 @@ def test_row_band_is_the_transposed_column_band(n1, n2, P, scheme):
 SHAPES = [(4, 1), (2, 2)]  # the horizontal strip shapes (256 rows each)
 
 
-def _check(torch, n1, n2, P, scheme, seed, alphabet=4, shape=(4, 1)):
+def _check(torch, n1, n2, P, scheme, seed, alphabet=4, shape=(4, 1), dense=False):
     rng = np.random.default_rng(seed)
     s1 = rng.integers(1, alphabet + 1, n1).astype(np.int8)
     s2 = rng.integers(1, alphabet + 1, n2).astype(np.int8)
-    tb = nw_bands.LocalTBands(n1, n2, P, shape=shape)
+    tb = nw_bands.LocalTBands(n1, n2, P, shape=shape, dense_polls=dense)
     try:
         score = tb.fill(torch.from_numpy(s1).cuda(), torch.from_numpy(s2).cuda(), scheme)
         full = oracle.fill(s1, s2, scheme)
@@ -87,6 +87,30 @@ def test_local_tbands_vs_oracle(torch_gpu, n1, n2, P, scheme, shape):
     in int8) and the compare forms (UNIT: match - mismatch == 1, GEN: (2,-1,-2)); both
     strip shapes ((2, 2): the band's last row may sit in either compute wave's ring)."""
     _check(torch_gpu, n1, n2, P, scheme, n1 * 31 + n2 + P, shape=shape)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n1,n2,P", [(300, 200, 2), (1000, 777, 3), (64 * 37 + 5, 999, 5), (1, 513, 2),
+                                     (2000, 20, 8)])
+@pytest.mark.parametrize("scheme", [(1, 0, -1), (2, -1, -2)])
+def test_local_tbands_dense_polls(torch_gpu, n1, n2, P, scheme):
+    """NW_TBAND_DENSE_POLLS (the long-chain poll policy, s_sleep 1 between polls): the same
+    bands, bit-exact."""
+    _check(torch_gpu, n1, n2, P, scheme, n1 * 17 + n2 + P, dense=True)
+
+
+def test_dense_poll_policy():
+    """bench.py --tband-polls auto: dense from chains of DENSE_POLL_STRIPS strips of 256 rows
+    (N = 8 at 65536 rows per GPU), sparse below; explicit choices win."""
+    import argparse
+    a = argparse.Namespace(tband_polls="auto")
+    assert not nw_bands.tband_dense(a, 2 * 65536) and not nw_bands.tband_dense(a, 4 * 65536)
+    assert nw_bands.tband_dense(a, 8 * 65536) and not nw_bands.tband_dense(a, 65536)
+    assert nw_bands.tband_dense(argparse.Namespace(tband_polls="dense"), 256)
+    assert not nw_bands.tband_dense(argparse.Namespace(tband_polls="sparse"), 8 * 65536)
+    assert not nw_bands.tband_dense(argparse.Namespace(), 2 * 65536)
+    with pytest.raises(ValueError):
+        nw_bands.tband_dense(argparse.Namespace(tband_polls="fast"), 1)
 
 
 @pytest.mark.gpu
@@ -175,6 +199,15 @@ def test_tband_refusals(torch_gpu):
             if st != nwhip.NW_OK:
                 raise nwhip.NwError(st, "nw_fill_tband_async")
         assert e.value.status == nwhip.NW_ERR_UNSUPPORTED
+        with pytest.raises(nwhip.NwError) as e:  # unknown nw_tband.flags bits
+            lib_p = nwhip.params((1, 0, -1))
+            st = nwhip.lib().nw_fill_tband_async(ctx._h, ctypes.c_void_p(s1.data_ptr()), n1,
+                                                 ctypes.c_void_p(s2.data_ptr()), n2, ctypes.byref(lib_p),
+                                                 ctypes.byref(nwhip.NwTBand(None, None, 1, 2, 0)),
+                                                 ctypes.c_void_p(tab.data_ptr()), tab.shape[1], None)
+            if st != nwhip.NW_OK:
+                raise nwhip.NwError(st, "nw_fill_tband_async")
+        assert e.value.status == nwhip.NW_ERR_ARG
         for sub, nc in [(1, 4), (2, 1), (1, 1), (2, 4), (4, 2)]:  # 256-row (4, 1) / (2, 2) strips only
             with pytest.raises(nwhip.NwError) as e:
                 ctx.fill_tband(s1, s2, tab, substrips=sub, strip_waves=nc)

@@ -19,6 +19,7 @@ ap.add_argument("--n2", type=int, default=65536)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--flags", type=int, default=0, help="nw_params.flags (513 = 0x201: timing only + no store waves, the compute pace)")
 ap.add_argument("--shape", default="4,1", help="horizontal strip shape C,NC: 4,1 or 2,2")
+ap.add_argument("--dense", action="store_true", help="NW_TBAND_DENSE_POLLS (follower polls with s_sleep 1)")
 ap.add_argument("--vertical", default="4:1,2:2", help="vertical-strip shapes to time beside it ('' = none)")
 args = ap.parse_args()
 SC, SNC = (int(x) for x in args.shape.split(","))
@@ -43,7 +44,7 @@ tag = [0]
 
 def tband():
     tag[0] += 1
-    ctx.fill_tband(s1, s2, tab, tag=tag[0], flags=args.flags, substrips=SC, strip_waves=SNC)
+    ctx.fill_tband(s1, s2, tab, tag=tag[0], flags=args.flags, substrips=SC, strip_waves=SNC, dense_polls=args.dense)
 
 
 timed(tband)

@@ -16,6 +16,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--n1", type=int, default=524288)
 ap.add_argument("--n2", default="16384,65536")
 ap.add_argument("--shape", default="4,1", help="horizontal strip shape C,NC: 4,1 or 2,2")
+ap.add_argument("--dense", action="store_true", help="NW_TBAND_DENSE_POLLS (follower polls with s_sleep 1)")
 args = ap.parse_args()
 SC, SNC = (int(x) for x in args.shape.split(","))
 ctx = nwhip.Context(0)
@@ -25,11 +26,11 @@ for n2 in [int(x) for x in args.n2.split(",")]:
     tab = nwhip.Context.alloc_table(args.n1, n2)
     nstrips = -(-n2 // 256)
     tr = torch.zeros(nstrips * 24, dtype=torch.int64, device="cuda")
-    ctx.fill_tband(s1, s2, tab, tag=1, substrips=SC, strip_waves=SNC)
+    ctx.fill_tband(s1, s2, tab, tag=1, substrips=SC, strip_waves=SNC, dense_polls=args.dense)
     ctx.set_trace(tr)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    ctx.fill_tband(s1, s2, tab, tag=2, substrips=SC, strip_waves=SNC)
+    ctx.fill_tband(s1, s2, tab, tag=2, substrips=SC, strip_waves=SNC, dense_polls=args.dense)
     e1.record()
     torch.cuda.synchronize()
     ctx.set_trace(None)
