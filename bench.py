@@ -73,7 +73,7 @@ def parse():
                          "nw_bands.TBAND_SHAPE)")
     ap.add_argument("--tband-polls", choices=["auto", "dense", "sparse"], default="auto",
                     help="N>1 horizontal-strip row bands: follower polls with s_sleep 1 (dense) or 64 "
-                         "(sparse); auto = dense for chains of 1200+ strips, i.e. N = 8 (nw_bands.tband_dense)")
+                         "(sparse); auto = dense for chains of 512+ strips, i.e. N >= 2 (nw_bands.tband_dense)")
     ap.add_argument("--kernel", type=int, default=0,
                     help="0 auto, 1 anti-diagonal strips, 2 row-scan panels (nw_params.kernel)")
     ap.add_argument("--col-width", type=int, default=65536,

@@ -764,17 +764,19 @@ int nw_fill_tband_async(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t 
             return e != nullptr && e[0] == '1';
         }();
         a.tr_store_pub = compute_pub && tNC == 1 ? 0 : 1;  // ((2, 2): the store waves publish)
-        // the band's unfed leading strip (band 0's strip 0: the whole chain's leader)
-        // sleeps 8 x 64 clocks per 64-step iteration (~8 %): followers that run 1-2 %
-        // slower for a while then keep up instead of delaying every strip below them
-        // (mean strip-to-strip lag 16.3-17.4 -> 12.5 us, leader 25.8 -> 27.5-28.0 ms;
-        // profiles/r06f_lead_sleep.txt); NW_LEAD_SLEEP overrides (A/B, 0 = off)
-        static const int lead_sleep = [] {
-            const char *e = std::getenv("NW_LEAD_SLEEP");
-            return e != nullptr ? std::atoi(e) : kTbandLeadSleep;
-        }();
-        a.lead_sleep = tNC == 1 ? lead_sleep : 0;
+        // With sparse polls the band's unfed leading strip (band 0's strip 0: the whole
+        // chain's leader) sleeps 8 x 64 clocks per 64-step iteration (~8 %): followers that
+        // run 1-2 % slower for a while then keep up instead of delaying every strip below
+        // them (mean strip-to-strip lag 16.3-17.4 -> 12.5 us, leader 25.8 -> 27.0-28.0 ms;
+        // profiles/r06f_lead_sleep.txt).  Dense polls slow the leader by themselves and
+        // need no throttle (lag 10.0 us at a leader of 28.0-28.5 ms with none, 29.7-29.8
+        // with 8: profiles/r06n_lead_dense.txt).  NW_LEAD_SLEEP overrides both (A/B).
         a.tr_dense = (tb->flags & NW_TBAND_DENSE_POLLS) != 0 ? 1 : 0;
+        static const int lead_env = [] {
+            const char *e = std::getenv("NW_LEAD_SLEEP");
+            return e != nullptr ? std::atoi(e) : -1;
+        }();
+        a.lead_sleep = tNC != 1 ? 0 : lead_env >= 0 ? lead_env : a.tr_dense ? 0 : kTbandLeadSleep;
     }
     if (nw::launch_fill(a, tC, tNC, (int)s.waves, stream) != hipSuccess) return NW_ERR_HIP;
     if (nw::launch_tband_edges(tb->feed_in, d_t, pitch, n1, R + 1, p->gap, tb->row0, stream) != hipSuccess)

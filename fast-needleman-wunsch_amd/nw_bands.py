@@ -709,12 +709,12 @@ CYCLE_ALT_BLOCKS = 2
 
 
 # Follower polls of the horizontal sweep (NW_TBAND_DENSE_POLLS; DESIGN.md section 5,
-# profiles/r06l_poll_sleep.txt): with the chain's leader throttled, s_sleep 1 polls give a
-# mean strip-to-strip lag of 9.9-10.3 us against 12.2-12.5 for s_sleep 64, but slow the
-# leader (29.4-30.0 vs 26.8-27.2 ms): they pay for chains longer than the break-even of
-# 2.4-2.9 ms / 2.2-2.5 us = 960-1300 strips of 256 rows -- N = 8 at 65536 rows per GPU
-# (2048 strips: -1.7 to -2.7 ms per fill), not N = 4 (1024: even).
-DENSE_POLL_STRIPS = 1200
+# profiles/r06l_poll_sleep.txt, r06n_lead_dense.txt): s_sleep 1 polls (which need no leader
+# throttle) give a mean strip-to-strip lag of 10.0 us at a leader of 28.0-28.5 ms, against
+# 12.2-12.5 us at 26.8-27.2 ms for s_sleep 64 with the throttled leader: they pay for chains
+# longer than the break-even of ~1.25 ms / 2.4 us = ~520 strips of 256 rows -- from N = 2
+# (512 strips: even) on; a band alone (256 strips) keeps sparse polls.
+DENSE_POLL_STRIPS = 512
 
 
 def tband_dense(args, n2: int) -> bool:

@@ -410,9 +410,10 @@ int nw_fill_colband_async(nw_ctx *ctx, const int8_t *d_s1, int64_t n1, const int
 /* nw_tband.flags */
 enum {
     /* the band's waiting strips poll their feed with s_sleep 1 instead of s_sleep 64
-       between polls: a shorter strip-to-strip lag (9.9-10.3 vs 12.2-12.5 us) at a
-       slower leading strip (29.4-30.0 vs 26.8-27.2 ms) -- the better choice for chains
-       of more than ~1200 strips (8 bands of 65536 rows) */
+       between polls (and the chain's leader is not throttled): a shorter strip-to-strip
+       lag (10.0 vs 12.2-12.5 us) at a slower leading strip (28.0-28.5 vs 26.8-27.2 ms) --
+       the better choice for chains of more than ~520 strips (2+ bands of 65536 rows;
+       DESIGN.md section 5) */
     NW_TBAND_DENSE_POLLS = 1
 };
 typedef struct nw_tband {

@@ -101,10 +101,11 @@ def test_local_tbands_dense_polls(torch_gpu, n1, n2, P, scheme):
 
 def test_dense_poll_policy():
     """bench.py --tband-polls auto: dense from chains of DENSE_POLL_STRIPS strips of 256 rows
-    (N = 8 at 65536 rows per GPU), sparse below; explicit choices win."""
+    (N >= 2 at 65536 rows per GPU), sparse below; explicit choices win."""
     import argparse
     a = argparse.Namespace(tband_polls="auto")
-    assert not nw_bands.tband_dense(a, 2 * 65536) and not nw_bands.tband_dense(a, 4 * 65536)
+    assert nw_bands.tband_dense(a, 2 * 65536) and nw_bands.tband_dense(a, 4 * 65536)
+    assert not nw_bands.tband_dense(a, 65536) and not nw_bands.tband_dense(a, 65536 + 65535)
     assert nw_bands.tband_dense(a, 8 * 65536) and not nw_bands.tband_dense(a, 65536)
     assert nw_bands.tband_dense(argparse.Namespace(tband_polls="dense"), 256)
     assert not nw_bands.tband_dense(argparse.Namespace(tband_polls="sparse"), 8 * 65536)
