@@ -109,7 +109,7 @@ def test_dense_poll_policy():
     assert nw_bands.tband_dense(a, 8 * 65536) and not nw_bands.tband_dense(a, 65536)
     assert nw_bands.tband_dense(argparse.Namespace(tband_polls="dense"), 256)
     assert not nw_bands.tband_dense(argparse.Namespace(tband_polls="sparse"), 8 * 65536)
-    assert not nw_bands.tband_dense(argparse.Namespace(), 2 * 65536)
+    assert nw_bands.tband_dense(argparse.Namespace(), 2 * 65536) and not nw_bands.tband_dense(argparse.Namespace(), 65536)
     with pytest.raises(ValueError):
         nw_bands.tband_dense(argparse.Namespace(tband_polls="fast"), 1)
 
