@@ -548,10 +548,13 @@ __device__ __forceinline__ Blk make_blk(const FillArgs &A, int t) {
 }
 
 // Compute wave j of strip B.pk.
-template <int C, int NC, int MODE>
+template <int C, int NC, int MODE, bool TRACE>
 __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restrict__ lds, const Blk &B,
                                               int j, int lane) {
     const int p = B.pk;
+    // the debug trace (FillArgs::trace) exists only in the TRACE build of the kernel:
+    // its stamps and counters otherwise hold ~20 SGPRs for the whole strip loop
+    uint64_t *const trace_p = TRACE ? A.trace : nullptr;
     typedef Lay<C, NC> L;
     constexpr bool SW = is_sw<MODE>();
     const int32_t gap = A.gap;
@@ -752,8 +755,8 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
         constexpr int GISS = (CONS + GPD) % NB;        // (it + GPD) % NB
         constexpr int HALF = CONS & 1;                 // it % 2
         constexpr bool RAMP = decltype(ramp_c)::value;
-        const bool traced = A.trace != nullptr && it == nblocks / 2;
-        if (A.trace != nullptr) {
+        const bool traced = trace_p != nullptr && it == nblocks / 2;
+        if (trace_p != nullptr) {
             if (it == nblocks / 4) tq1 = __builtin_amdgcn_s_memrealtime();
             if (traced) tmid = __builtin_amdgcn_s_memrealtime();
             F.trace_pub = it == nblocks / 2 + 1;
@@ -812,10 +815,10 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
         load_packs(pkp, it + PD, lane, pkb[ISS]);
         const int b = it - 1;  // block whose right column this iteration publishes
         uint64_t *gp = (b >= 0 && b < nblocks) ? gout + (int64_t)b * 64 + lane : gscr;
-        const uint64_t ti0 = A.trace != nullptr ? __builtin_amdgcn_s_memtime() : 0;
+        const uint64_t ti0 = trace_p != nullptr ? __builtin_amdgcn_s_memtime() : 0;
         run_iter<C, NC, MODE, RAMP, HALF>(lds, it, pkb[CONS], msp, mmp, gap, S, ctr, rd, b, gp, tagw,
                                           O, A.ctrl, F, lane);
-        if (A.trace != nullptr) tin += __builtin_amdgcn_s_memtime() - ti0;
+        if (trace_p != nullptr) tin += __builtin_amdgcn_s_memtime() - ti0;
         ctr_store(ctr + 2, it + 1);  // iterations done (feed-ring space for wave j-1)
         dead = F.dead;
     };
@@ -837,8 +840,8 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
     ctr_store(ctr, kDone);
     ctr_store(ctr + 1, kDone);
     ctr_store(ctr + 2, kDone);
-    if (A.trace != nullptr && lane == 0) {
-        uint64_t *tr = A.trace + (int64_t)(B.pq - A.strip0) * kTraceWords;
+    if (trace_p != nullptr && lane == 0) {
+        uint64_t *tr = trace_p + (int64_t)(B.pq - A.strip0) * kTraceWords;
         if (j == 0) {
             tr[0] = tstart;
             tr[2] = F.nslow;
@@ -871,7 +874,7 @@ __device__ __forceinline__ void compute_strip(const FillArgs &A, char *__restric
 // loads and its waits are LDS waits.  Ring space: row r overwrites row r - 256,
 // read by wave 0's iteration (r - 256) / 64, so the wave waits for wave 0's
 // iterations-done counter.  Serial polls (nw_dev.h wait_chunk): one load in flight.
-template <int C, int NC>
+template <int C, int NC, bool TRACE>
 __device__ __forceinline__ void feed_strip(const FillArgs &A, char *__restrict__ lds, const Blk &B, int lane) {
     typedef Lay<C, NC> L;
     int32_t *ctl = (int32_t *)(lds + L::kCtl);
@@ -890,7 +893,7 @@ __device__ __forceinline__ void feed_strip(const FillArgs &A, char *__restrict__
     uint32_t idle = 0;
     // debug trace (words 19..23): ring-space wait total, the longest no-data streak,
     // the row it waited for, when it ended, number of streaks over 100 us
-    const bool traced = A.trace != nullptr;
+    const bool traced = TRACE && A.trace != nullptr;
     uint64_t t_ring = 0, t_max = 0, t_max_end = 0, n_long = 0;
     int32_t r_max = 0;
     while (avail < nrow) {
@@ -1268,7 +1271,7 @@ __device__ __forceinline__ void store_strip_tr(const FillArgs &A, char *__restri
 // gathered with 4 conflict-free ds_read_b32 (the value of column a of row f + r
 // was computed at step f + r + a: record group (f+r+a)/4, word (f+r+a)%4).
 // Rows go in batches of kBatch dealt round robin to the kSPR store waves.
-template <int NC>
+template <int NC, bool TRACE>
 __device__ __forceinline__ void store_strip_grp(const FillArgs &A, char *__restrict__ lds, const Blk &B,
                                                 int j, int q, int lane) {
     const int p = B.pk;
@@ -1328,7 +1331,7 @@ __device__ __forceinline__ void store_strip_grp(const FillArgs &A, char *__restr
         return;
     }
     // debug trace (store wave 0 of ring 0): cycles waiting for rows / issuing stores
-    const bool trace = A.trace != nullptr && j == 0 && q == 0;
+    const bool trace = TRACE && A.trace != nullptr && j == 0 && q == 0;
     uint64_t tw = 0, ts = 0;
     int32_t avail = 0;
     // batch f complete in the ring: left halves of rows < min(f + BATCH, nrows)
@@ -1502,11 +1505,21 @@ constexpr bool sw_shape(int c, int nc) {
            (c == 2 && nc == 4);
 }
 
+// Kernel kinds: which two copies of the compute loop a kernel holds (the table form
+// and a compare form; the choice between them is made on the device, from nprof).
+// One kernel per kind rather than one holding every mode: each further copy of the
+// unrolled loop, and the debug trace's stamps, raise the SGPR pressure of the whole
+// kernel, which spills at the iteration boundaries (round 6: the generic (2, 2)
+// kernel 485 spilled SGPRs with four modes and the trace, 136 for one kind without).
+enum StripKind { KIND_GEN = 0, KIND_UNIT = 1, KIND_SW = 2 };
+
 // Persistent grid of workgroups of NC compute waves (0 .. NC-1) and NC*kSPR
 // store waves (wave NC + b serves ring b % NC).
-template <int C, int NC, bool UNIT>
+template <int C, int NC, int KIND, bool TRACE>
 __global__ __launch_bounds__((64 * Lay<C, NC>::kWaves)) void nw_fill_strips(FillArgs A) {
     typedef Lay<C, NC> L;
+    static_assert(KIND != KIND_SW || sw_shape(C, NC), "Smith-Waterman kernel of a non-SW shape");
+    static_assert(!L::kHalf || KIND == KIND_SW, "half-word rings hold Smith-Waterman cells only");
     __shared__ __attribute__((aligned(16))) char lds[L::kBytes];
     int32_t *ctl = (int32_t *)(lds + L::kCtl);
     const int lane = threadIdx.x & 63;
@@ -1528,33 +1541,26 @@ __global__ __launch_bounds__((64 * Lay<C, NC>::kWaves)) void nw_fill_strips(Fill
             // table form when the launch allows it (scores fit int8) and s1 has
             // at most kMaxPerm distinct characters (nw_charmap), else compares
             const uint32_t np = __builtin_amdgcn_readfirstlane(ctrl_load(A.nprof));
-            bool sw_done = false;
-            if constexpr (sw_shape(C, NC) && !UNIT) {  // (SW launches use the generic kernel)
-                if (A.sw) {
-                    if (A.perm != 0 && np <= kMaxPerm)
-                        compute_strip<C, NC, SUB_PERM_SW>(A, lds, B, wave, lane);
-                    else
-                        compute_strip<C, NC, SUB_GEN_SW>(A, lds, B, wave, lane);
-                    sw_done = true;
-                }
-            }
-            if constexpr (L::kHalf) {
-                // half-word rings hold Smith-Waterman cells only (the host refuses NW)
-            } else if (sw_done) {
-            } else if (A.perm != 0 && np <= kMaxPerm) {
-                compute_strip<C, NC, SUB_PERM>(A, lds, B, wave, lane);
-            } else if (UNIT) {
-                compute_strip<C, NC, SUB_UNIT>(A, lds, B, wave, lane);
+            const bool perm = A.perm != 0 && np <= kMaxPerm;
+            if constexpr (KIND == KIND_SW) {
+                if (perm)
+                    compute_strip<C, NC, SUB_PERM_SW, TRACE>(A, lds, B, wave, lane);
+                else
+                    compute_strip<C, NC, SUB_GEN_SW, TRACE>(A, lds, B, wave, lane);
+            } else if (perm) {
+                compute_strip<C, NC, SUB_PERM, TRACE>(A, lds, B, wave, lane);
+            } else if constexpr (KIND == KIND_UNIT) {
+                compute_strip<C, NC, SUB_UNIT, TRACE>(A, lds, B, wave, lane);
             } else {
-                compute_strip<C, NC, SUB_GEN>(A, lds, B, wave, lane);
+                compute_strip<C, NC, SUB_GEN, TRACE>(A, lds, B, wave, lane);
             }
         } else if (L::kFeeder && wave == L::kWaves - 1) {
-            feed_strip<C, NC>(A, lds, B, lane);
+            feed_strip<C, NC, TRACE>(A, lds, B, lane);
         } else {
             const int b = wave - NC;
             if constexpr (L::kGrp) {
-                store_strip_grp<NC>(A, lds, B, b % NC, b / NC, lane);
-            } else if constexpr ((C == 4 && NC == 1) || (C == 2 && NC == 2)) {
+                store_strip_grp<NC, TRACE>(A, lds, B, b % NC, b / NC, lane);
+            } else if constexpr (((C == 4 && NC == 1) || (C == 2 && NC == 2)) && KIND != KIND_SW) {
                 if (A.tr != 0)
                     store_strip_tr<C, NC>(A, lds, B, b % NC, b / NC, lane);  // (row band in horizontal strips)
                 else
@@ -1566,15 +1572,32 @@ __global__ __launch_bounds__((64 * Lay<C, NC>::kWaves)) void nw_fill_strips(Fill
         __syncthreads();  // the rings and counters are reused by the next strip
     }
 }
+// The kernel of a launch: Smith-Waterman, or NW with match - mismatch = 1 (the
+// compare form is then one add-with-carry), or NW generic; the trace build (only of
+// the generic and SW kinds: a unit scheme's trace runs the generic kernel, whose
+// table form is the same code) when FillArgs::trace is set.
 template <int C, int NC>
 static void launch_c(const FillArgs &a, int grid, hipStream_t s) {
     const dim3 block(64 * Lay<C, NC>::kWaves);
-    if constexpr (Lay<C, NC>::kHalf)  // (Smith-Waterman only)
-        hipLaunchKernelGGL((nw_fill_strips<C, NC, false>), dim3(grid), block, 0, s, a);
-    else if (a.match - a.mismatch == 1 && !a.sw)
-        hipLaunchKernelGGL((nw_fill_strips<C, NC, true>), dim3(grid), block, 0, s, a);
-    else
-        hipLaunchKernelGGL((nw_fill_strips<C, NC, false>), dim3(grid), block, 0, s, a);
+    const bool tr = a.trace != nullptr;
+    if constexpr (sw_shape(C, NC)) {
+        if (a.sw) {
+            if (tr)
+                hipLaunchKernelGGL((nw_fill_strips<C, NC, KIND_SW, true>), dim3(grid), block, 0, s, a);
+            else
+                hipLaunchKernelGGL((nw_fill_strips<C, NC, KIND_SW, false>), dim3(grid), block, 0, s, a);
+            return;
+        }
+    }
+    if constexpr (!Lay<C, NC>::kHalf) {  // (the host refuses NW on half-word rings)
+        if (a.sw) return;                // (and SW on the shapes without an SW kernel)
+        if (tr)
+            hipLaunchKernelGGL((nw_fill_strips<C, NC, KIND_GEN, true>), dim3(grid), block, 0, s, a);
+        else if (a.match - a.mismatch == 1)
+            hipLaunchKernelGGL((nw_fill_strips<C, NC, KIND_UNIT, false>), dim3(grid), block, 0, s, a);
+        else
+            hipLaunchKernelGGL((nw_fill_strips<C, NC, KIND_GEN, false>), dim3(grid), block, 0, s, a);
+    }
 }
 
 }  // namespace nw
