@@ -1,12 +1,12 @@
 #!/bin/bash
-# A/B of two builds of libnwhip on one box, alternating A B A B (run from the repo root):
+# A/B of builds of libnwhip on one box, alternating A B .. A B .. (run from the repo root):
 #   SW 64k fill (config 5's fill), SW strip 0 alone, config-4 rank-7 band alone
 #   (horizontal), two chained horizontal bands of 524288 x 32768 on one GPU.
-# Usage: bash tools/ab_libs.sh <outfile> <libA> <libB>
+# Usage: bash tools/ab_libs.sh <outfile> <libA> <libB> [<libC> ...]
 set -o pipefail
 OUT=$1
-A=$2
-B=$3
+shift
+LIBS="$*"
 : > "$OUT"
 run() {  # lib, label, command...
     local lib=$1 lab=$2
@@ -15,7 +15,7 @@ run() {  # lib, label, command...
     NWHIP_LIB=$lib timeout -k 10 180 "$@" >> "$OUT" 2>&1 || { echo "FAILED rc=$? ($lab $*)" >> "$OUT"; exit 1; }
 }
 for pass in 1 2; do
-    for lib in "$A" "$B"; do
+    for lib in $LIBS; do
         lab="pass$pass $(basename "$lib")"
         run "$lib" "$lab" python -u tools/sw_attr.py --n1 65536 --n2 65536 --reps 5
         run "$lib" "$lab" python -u tools/sw_attr.py --reps 5
