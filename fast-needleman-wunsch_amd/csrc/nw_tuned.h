@@ -11,11 +11,11 @@ struct TunedShape {
     int c, nc;         // columns per lane, chained compute waves per strip / panel
 };
 constexpr TunedShape kTuned[] = {
-    {0.0, 1, 2, 1},  // best at 4096^2: 46 GCUPS
-    {67129345.0, 1, 2, 2},  // best at 16384^2: 203 GCUPS
-    {536920065.0, 1, 2, 2},  // best at 32768^2: 403 GCUPS
-    {2147581953.0, 1, 4, 1},  // best at 65536^2: 701 GCUPS
-    {8590131201.0, 1, 1, 4},  // best at 131072^2: 1027 GCUPS
-    {34360131585.0, 2, 4, 4},  // best at 262144^2: 1463 GCUPS
+    {0.0, 1, 4, 1},  // best at 4096^2: 47 GCUPS
+    {67129345.0, 1, 2, 2},  // best at 16384^2: 211 GCUPS
+    {536920065.0, 1, 2, 2},  // best at 32768^2: 421 GCUPS
+    {2147581953.0, 1, 2, 2},  // best at 65536^2: 760 GCUPS
+    {8590131201.0, 2, 2, 4},  // best at 131072^2: 1052 GCUPS
+    {34360131585.0, 2, 4, 4},  // best at 262144^2: 1534 GCUPS
 };
 }  // namespace nw

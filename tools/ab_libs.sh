@@ -22,7 +22,7 @@ for pass in 1 2; do
         run "$lib" "$lab" python -u tools/band_alone.py --rank 7 --sweep horizontal --reps 3
         run "$lib" "$lab" python -u tools/local_bands_time.py --P 2 --only horizontal --reps 3
         # AB_TRACE=1: the band's strip timeline too (hop, mean lag; the TRACE build of the kernel)
-        if [ "${AB_TRACE:-0}" = 1 ]; then run "$lib" "$lab" python -u tools/tband_trace.py --n2 65536; fi
+        if [ "${AB_TRACE:-0}" = 1 ]; then run "$lib" "$lab" python -u tools/tband_trace.py --n2 65536 ${AB_TRACE_ARGS:-}; fi
     done
 done
 echo done >> "$OUT"
