@@ -776,7 +776,7 @@ int nw_fill_tband_async(nw_ctx *c, const int8_t *d_s1, int64_t n1, const int8_t 
             const char *e = std::getenv("NW_LEAD_SLEEP");
             return e != nullptr ? std::atoi(e) : -1;
         }();
-        a.lead_sleep = tNC != 1 ? 0 : lead_env >= 0 ? lead_env : a.tr_dense ? 0 : kTbandLeadSleep;
+        a.lead_sleep = lead_env >= 0 ? lead_env : tNC != 1 ? 0 : a.tr_dense ? 0 : kTbandLeadSleep;
     }
     if (nw::launch_fill(a, tC, tNC, (int)s.waves, stream) != hipSuccess) return NW_ERR_HIP;
     if (nw::launch_tband_edges(tb->feed_in, d_t, pitch, n1, R + 1, p->gap, tb->row0, stream) != hipSuccess)
